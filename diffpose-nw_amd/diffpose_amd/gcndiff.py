@@ -1,0 +1,227 @@
+"""HipGCNdiff — the GCNdiff denoiser as a handle on the HIP library.
+
+Mirrors the reference model's construction and call surface
+(``GCNdiff(adj, config)``, ``load_state_dict(states[0])``, ``model(x, mask, t, cemd)``;
+reference ``models/gcndiff.py:55-113``, ``runners/diffpose_frame.py:118-132``) so a
+caller can swap it in for the DataParallel-wrapped torch module at inference.
+All compute runs in libdpk.so on the GPU; torch is used only for device memory
+and the current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .schedule import alpha_bar_table
+from .weights import HID, N_HEAD, N_LAYERS, N_PTS, COORDS, normalize_state_dict
+
+# 16 skeleton edges of the runner (runners/diffpose_frame.py:120-124)
+H36M_EDGES = ((0, 1), (1, 2), (2, 3), (0, 4), (4, 5), (5, 6), (0, 7), (7, 8), (8, 9), (9, 10),
+              (8, 11), (11, 12), (12, 13), (8, 14), (14, 15), (15, 16))
+
+
+def adj_mx_from_edges(num_pts: int = N_PTS, edges=H36M_EDGES) -> np.ndarray:
+    """Row-normalised D^-1 (A_sym + I) as float32 (reference models/GraFormer.py:32-44, sparse=False)."""
+    a = np.zeros((num_pts, num_pts), dtype=np.float32)
+    for i, j in np.asarray(edges, dtype=np.int64).reshape(-1, 2):
+        a[i, j] = 1.0
+        a[j, i] = 1.0
+    a += np.eye(num_pts, dtype=np.float32)
+    inv = np.power(a.sum(1, dtype=np.float32), -1).astype(np.float32)
+    inv[np.isinf(inv)] = 0.0
+    return (inv[:, None] * a).astype(np.float32)
+
+
+def _f32p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _dev_index(device) -> int:
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"HipGCNdiff runs on a HIP device, got {d}")
+    return torch.cuda.current_device() if d.index is None else d.index
+
+
+def _model_dims(config):
+    if config is None:
+        return HID, N_LAYERS, N_HEAD, N_PTS, tuple(COORDS)
+    m = getattr(config, "model", config)
+    return (int(m.hid_dim), int(m.num_layer), int(m.n_head), int(m.n_pts), tuple(int(c) for c in m.coords_dim))
+
+
+class HipGCNdiff:
+    """GCNdiff(adj, config) on MI355X.  ``model(x, mask, t, cemd) -> eps`` like the reference."""
+
+    def __init__(self, adj, config=None, device=None):
+        hid, nl, nh, npts, coords = _model_dims(config)
+        self.device = torch.device("cuda", _dev_index(device))
+        L = _lib.lib()
+        cfg = _lib.DpkConfig(hid, nl, nh, npts, coords[0], coords[1], self.device.index)
+        h = ctypes.c_void_p()
+        rc = L.dpk_create(ctypes.byref(cfg), ctypes.byref(h))
+        _lib.check(None, "dpk_create", rc)
+        self._h = h
+        self.n_pts = npts
+        adj = adj.detach().cpu().numpy() if torch.is_tensor(adj) else np.asarray(adj)
+        self.adj = np.ascontiguousarray(adj, dtype=np.float32)
+        if self.adj.shape != (npts, npts):
+            raise ValueError(f"adj must be ({npts},{npts}), got {self.adj.shape}")
+        _lib.check(h, "dpk_set_graph", L.dpk_set_graph(h, _f32p(self.adj)))
+        self._mask_key = None
+        self._sched_key = None
+        self.training = False
+
+    # -- nn.Module-like surface -------------------------------------------------------
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Accept the reference's states[0] (with/without 'module.'), torch tensors or numpy."""
+        sd = normalize_state_dict(state_dict)
+        names = list(sd.keys())
+        arrs = [np.ascontiguousarray(sd[k], dtype=np.float32) for k in names]
+        c_names = (ctypes.c_char_p * len(names))(*[k.encode() for k in names])
+        c_ptrs = (ctypes.POINTER(ctypes.c_float) * len(arrs))(*[_f32p(a) for a in arrs])
+        c_num = (ctypes.c_int64 * len(arrs))(*[a.size for a in arrs])
+        L = _lib.lib()
+        _lib.check(self._h, "dpk_load_weights", L.dpk_load_weights(self._h, c_names, c_ptrs, c_num, len(arrs)))
+        self._state = sd
+        return self
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise NotImplementedError("HipGCNdiff is inference-only (training is out of scope, SURVEY §8f f4)")
+        return self.eval()
+
+    def to(self, *a, **k):
+        return self
+
+    def cuda(self, *a, **k):
+        return self
+
+    def parameters(self):
+        return iter(())
+
+    # -- mask -----------------------------------------------------------------------
+    def set_mask(self, mask) -> None:
+        if mask is None:
+            m = np.ones(self.n_pts, dtype=np.uint8)
+        else:
+            mt = mask.detach().cpu() if torch.is_tensor(mask) else torch.as_tensor(np.asarray(mask))
+            if mt.dim() == 3 and mt.shape[0] != 1:
+                raise NotImplementedError("per-sample attention masks are not supported (the reference uses (1,1,17))")
+            m = mt.reshape(-1).numpy().astype(np.uint8)
+            if m.size != self.n_pts:
+                raise ValueError(f"mask must have {self.n_pts} key entries, got {m.size}")
+        m = np.ascontiguousarray(m)
+        L = _lib.lib()
+        _lib.check(self._h, "dpk_set_mask", L.dpk_set_mask(self._h, m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+
+    def _sync_mask(self, mask) -> None:
+        key = None if mask is None else (id(mask), getattr(mask, "_version", 0))
+        if key != self._mask_key or key is None:
+            self.set_mask(mask)
+            self._mask_key = key
+
+    # -- schedule -------------------------------------------------------------------
+    def set_schedule(self, seq, betas, eta: float = 0.0) -> None:
+        """Bind seq / betas / eta (cached: re-uploaded only when they change)."""
+        b = betas.detach().cpu().numpy() if torch.is_tensor(betas) else np.asarray(betas)
+        b = np.ascontiguousarray(b, dtype=np.float32)
+        seq = [int(s) for s in seq]
+        key = (tuple(seq), b.tobytes(), float(eta))
+        if key == self._sched_key:
+            return
+        abar = np.ascontiguousarray(alpha_bar_table(b))
+        cseq = (ctypes.c_int * len(seq))(*seq)
+        L = _lib.lib()
+        _lib.check(self._h, "dpk_set_schedule",
+                   L.dpk_set_schedule(self._h, _f32p(abar), abar.size, cseq, len(seq), ctypes.c_float(eta)))
+        self._sched_key = key
+        self.K = len(seq)
+
+    # -- compute --------------------------------------------------------------------
+    def _check_x(self, x):
+        if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32):
+            raise TypeError("x must be a float32 CUDA(HIP) tensor")
+        if x.dim() != 3 or x.shape[1] != self.n_pts or x.shape[2] != 5:
+            raise ValueError(f"x must be (N, {self.n_pts}, 5), got {tuple(x.shape)}")
+        if x.device != self.device:
+            raise ValueError(f"x on {x.device}, model on {self.device}")
+        return x.contiguous()
+
+    def forward(self, x, mask, t, cemd=0):
+        """eps = GCNdiff(x, mask, t) (models/gcndiff.py:101-113); ``cemd`` is unused there too."""
+        x = self._check_x(x)
+        n = x.shape[0]
+        t = torch.as_tensor(t, device=self.device).to(torch.float32).reshape(-1).contiguous()
+        if t.numel() == 1 and n != 1:
+            t = t.expand(n).contiguous()
+        if t.numel() != n:
+            raise ValueError(f"t must have {n} entries, got {t.numel()}")
+        self._sync_mask(mask)
+        eps = torch.empty_like(x)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L = _lib.lib()
+        _lib.check(self._h, "dpk_eps", L.dpk_eps(self._h, x.data_ptr(), t.data_ptr(), eps.data_ptr(), n, stream))
+        return eps
+
+    __call__ = forward
+
+    def sample(self, x, seq, betas, eta: float = 0.0, mask=None, seed: int = 0, trajectory: bool = False,
+               out=None):
+        """Run the whole DDIM loop on device.  Returns the final x, or (xs, x0s) stacks
+        ([K+1,N,17,5], [K,N,17,5]) when ``trajectory`` is set."""
+        x = self._check_x(x)
+        self.set_schedule(seq, betas, eta)
+        self._sync_mask(mask)
+        n = x.shape[0]
+        out = torch.empty_like(x) if out is None else out
+        xs = x0s = None
+        if trajectory:
+            xs = torch.empty((self.K + 1,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+            x0s = torch.empty((self.K,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L = _lib.lib()
+        rc = L.dpk_sample(self._h, x.data_ptr(), out.data_ptr(), xs.data_ptr() if xs is not None else None,
+                          x0s.data_ptr() if x0s is not None else None, n, ctypes.c_uint64(seed & (2**64 - 1)),
+                          stream)
+        _lib.check(self._h, "dpk_sample", rc)
+        if trajectory:
+            return xs, x0s
+        return out
+
+    def ddim_update(self, xt, et, step: int, seed: int = 0, want_x0: bool = True):
+        """x_{t-1} (and x0) from an external eps for schedule step ``step``."""
+        xt, et = xt.contiguous(), et.contiguous()
+        xn = torch.empty_like(xt)
+        x0 = torch.empty_like(xt) if want_x0 else None
+        stream = torch.cuda.current_stream(xt.device).cuda_stream
+        L = _lib.lib()
+        rc = L.dpk_ddim_update(self._h, xt.data_ptr(), et.data_ptr(), xn.data_ptr(),
+                               x0.data_ptr() if x0 is not None else None, xt.numel(), step,
+                               ctypes.c_uint64(seed & (2**64 - 1)), stream)
+        _lib.check(self._h, "dpk_ddim_update", rc)
+        return xn, x0
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            _lib.lib().dpk_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def GCNdiff(adj, config, device=None) -> HipGCNdiff:   # noqa: N802  (reference constructor name)
+    return HipGCNdiff(adj, config, device=device)

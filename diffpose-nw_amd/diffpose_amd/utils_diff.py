@@ -1,0 +1,72 @@
+"""Drop-in ``common/utils_diff.py``: get_beta_schedule, compute_alpha, generalized_steps.
+
+``generalized_steps(x, src_mask, seq, model, b, **kwargs) -> (xs, x0_preds)`` keeps
+the reference signature and return shape (reference ``common/utils_diff.py:46-68``):
+``xs`` is a list of K+1 tensors whose first element IS the input object, and
+``x0_preds`` a list of K tensors.
+
+* ``model`` a :class:`HipGCNdiff` → the whole loop runs as one persistent HIP kernel
+  (``dpk_sample``) writing the trajectory into two preallocated stacks.
+* any other callable ``model(xt, mask, t, cemd)`` → the loop runs on the host, each
+  step's DDIM update in the HIP ``dpk_ddim_update`` kernel.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .gcndiff import HipGCNdiff
+from .schedule import alpha_bar_table, get_beta_schedule, step_pairs  # noqa: F401  (re-exported)
+
+
+def compute_alpha(beta, t):
+    """(1 - cat([0], beta)).cumprod(0)[t+1] as (N,1,1) (common/utils_diff.py:40-43); host table."""
+    b = beta.detach().cpu().numpy() if torch.is_tensor(beta) else np.asarray(beta)
+    table = torch.from_numpy(alpha_bar_table(b))
+    idx = torch.as_tensor(t).long().cpu() + 1
+    out = table.index_select(0, idx).view(-1, 1, 1)
+    return out.to(beta.device) if torch.is_tensor(beta) else out
+
+
+def generalized_steps(x, src_mask, seq, model, b, **kwargs):
+    eta = float(kwargs.get("eta", 0))
+    seed = int(kwargs.get("seed", 0))
+    seq = [int(s) for s in seq]
+    with torch.no_grad():
+        if isinstance(model, HipGCNdiff):
+            xs_t, x0s_t = model.sample(x, seq, b, eta=eta, mask=src_mask, seed=seed, trajectory=True)
+            return [x] + [xs_t[k] for k in range(1, xs_t.shape[0])], [x0s_t[k] for k in range(x0s_t.shape[0])]
+        # generic callable: host loop, HIP DDIM update
+        upd = kwargs.get("updater")
+        if upd is None:
+            upd = HipGCNdiff.__new__(HipGCNdiff)
+            _init_schedule_only(upd, x.device)
+        upd.set_schedule(seq, b, eta)
+        n = x.size(0)
+        xs, x0s = [x], []
+        for step, (i, _j) in enumerate(step_pairs(seq)):
+            t = torch.full((n,), float(i), device=x.device)
+            et = model(xs[-1], src_mask, t, 0)
+            xn, x0 = upd.ddim_update(xs[-1], et, step, seed=seed)
+            x0s.append(x0)
+            xs.append(xn)
+        return xs, x0s
+
+
+def _init_schedule_only(obj: HipGCNdiff, device) -> None:
+    """A handle used only for its schedule table and the DDIM update kernel."""
+    import ctypes
+
+    from . import _lib
+    from .weights import COORDS, HID, N_HEAD, N_LAYERS, N_PTS
+
+    obj.device = torch.device(device)
+    L = _lib.lib()
+    cfg = _lib.DpkConfig(HID, N_LAYERS, N_HEAD, N_PTS, COORDS[0], COORDS[1], obj.device.index or 0)
+    h = ctypes.c_void_p()
+    _lib.check(None, "dpk_create", L.dpk_create(ctypes.byref(cfg), ctypes.byref(h)))
+    obj._h = h
+    obj.n_pts = N_PTS
+    obj._mask_key = None
+    obj._sched_key = None
+    obj.training = False

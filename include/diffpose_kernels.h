@@ -1,0 +1,112 @@
+/*
+ * diffpose_kernels.h — C ABI of the MI355X-native DiffPose DDIM sampler (libdpk.so).
+ *
+ * Drop-in boundary for the reference hot path (reference at nwicakson/diffpose-nw):
+ *   - the denoiser callable  GCNdiff.forward(x, mask, t, cemd) -> eps      models/gcndiff.py:101-113
+ *     (called once per step at common/utils_diff.py:58)
+ *   - the DDIM reverse loop  generalized_steps(x, src_mask, seq, model, b, eta)
+ *                                                                           common/utils_diff.py:46-68
+ *   - its caller             Diffpose.test_hyber                           runners/diffpose_frame.py:345-370
+ * The reference has no FFI of its own (pure PyTorch); these entry points are what a
+ * ctypes binding of that seam needs.  INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All tensor pointers are caller-owned DEVICE memory (fp32, row-major, contiguous)
+ *     on the device the handle was created for; work is enqueued on `stream`
+ *     (a hipStream_t, NULL = default stream) and is asynchronous.
+ *   - Poses are (N, 17, 5) uvxyz: N poses x 17 joints x 5 channels.
+ *   - Return value 0 = OK, negative = error (DPK_E_*); dpk_last_error() has the text.
+ *   - A handle is bound to one device and is not thread-safe: one handle per rank/thread.
+ */
+#ifndef DIFFPOSE_KERNELS_H
+#define DIFFPOSE_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPK_OK              0
+#define DPK_E_INVALID      -1   /* bad argument (null pointer, N<0, size mismatch)       */
+#define DPK_E_UNSUPPORTED  -2   /* model dims other than the compiled GCNdiff shape      */
+#define DPK_E_HIP          -3   /* HIP runtime error                                     */
+#define DPK_E_STATE        -4   /* weights / graph / schedule not set yet                */
+#define DPK_E_WEIGHTS      -5   /* unknown, missing or mis-sized state_dict entry        */
+
+typedef struct dpk_handle dpk_handle;
+
+/* GCNdiff hyper-parameters (configs/human36m_diffpose_uvxyz_*.yml model: section,
+ * emd_dim = 4*hid_dim per models/gcndiff.py:68).  The kernels are compiled for
+ * hid_dim 96, num_layer 5, n_head 4, n_pts 17, coords_dim [5,5]. */
+typedef struct {
+    int hid_dim;
+    int num_layers;
+    int n_head;
+    int n_pts;
+    int coords_in;
+    int coords_out;
+    int device;        /* HIP device ordinal */
+} dpk_config;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int dpk_version(void);
+
+/* Create a handle on cfg->device.  Replaces GCNdiff(adj, config) construction
+ * (models/gcndiff.py:55-99; runners/diffpose_frame.py:118-127). */
+int dpk_create(const dpk_config* cfg, dpk_handle** out);
+
+/* Dense n_pts x n_pts adjacency as passed to GCNdiff(adj, ...) (row-normalised,
+ * models/GraFormer.py:32-44).  Derives the Chebyshev terms T0..T2 of its
+ * normalised Laplacian once (models/ChebConv.py:90-130), instead of per call. */
+int dpk_set_graph(dpk_handle* h, const float* adj_host);
+
+/* Load a GCNdiff state_dict (keys as in models/gcndiff.py, with or without the
+ * DataParallel "module." prefix; runners/diffpose_frame.py:130-132).  Copies the n
+ * host arrays, repacks GEMM weights into MFMA fragment order and precomputes each
+ * layer's GraphNet Laplacian (models/GraFormer.py:174-178).  All keys required. */
+int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const* host_ptrs,
+                     const int64_t* numels, int n);
+
+/* Attention key mask, n_pts bytes (nonzero = attend).  Default all ones, the
+ * reference's src_mask (runners/diffpose_frame.py:39-40); zero entries take the
+ * masked_fill(-1e9) path of models/GraFormer.py:107-108. */
+int dpk_set_mask(dpk_handle* h, const uint8_t* mask_host);
+
+/* DDIM schedule.  alpha_bar: fp32 table (1-cat([0],betas)).cumprod(0), n_alpha = T+1
+ * entries (compute_alpha, common/utils_diff.py:40-43); seq: K timesteps in
+ * ascending order as built by test_hyber (runners/diffpose_frame.py:310-317);
+ * eta as in common/utils_diff.py:61-63.  Step scalars are evaluated in fp32 in
+ * the reference's operation order. */
+int dpk_set_schedule(dpk_handle* h, const float* alpha_bar, int n_alpha, const int* seq, int K, float eta);
+
+/* One denoiser evaluation eps = GCNdiff(x, mask, t) for N poses with a
+ * per-pose timestep t_dev[N] (float, as model(xt, mask, t.float(), 0)). */
+int dpk_eps(dpk_handle* h, const float* x_dev, const float* t_dev, float* eps_dev, int N, void* stream);
+
+/* The whole K-step reverse loop of generalized_steps for N poses in ONE
+ * persistent kernel (plus one timestep-embedding kernel).
+ *   x_dev   [N,17,5] input x (= xs[0])
+ *   out_dev [N,17,5] final sample xs[-1]
+ *   xs_dev  [K+1,N,17,5] or NULL: full trajectory xs (xs[0] copied from x_dev)
+ *   x0s_dev [K,N,17,5]   or NULL: x0_preds
+ *   seed: noise stream for eta > 0 (counter-based, not torch.randn_like). */
+int dpk_sample(dpk_handle* h, const float* x_dev, float* out_dev, float* xs_dev, float* x0s_dev,
+               int N, uint64_t seed, void* stream);
+
+/* One DDIM update for an externally computed eps (generic model callables):
+ * the per-element body of common/utils_diff.py:59-65 for schedule step `step`
+ * (0 = first executed step, t = seq[K-1]).  x0_out may be NULL. */
+int dpk_ddim_update(dpk_handle* h, const float* xt_dev, const float* eps_dev, float* xnext_dev,
+                    float* x0_dev, int64_t n_elems, int step, uint64_t seed, void* stream);
+
+/* Poses per workgroup of the sampler kernel and its static LDS bytes (for docs/bench). */
+int dpk_kernel_geometry(int* poses_per_workgroup, int* threads_per_workgroup, int* lds_bytes);
+
+const char* dpk_last_error(const dpk_handle* h);
+void dpk_destroy(dpk_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIFFPOSE_KERNELS_H */

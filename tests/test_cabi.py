@@ -1,0 +1,69 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/*.h declares.
+
+No compute call is made here (there is no GPU in the build container); argument
+validation paths that return before touching the device are exercised.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from diffpose_amd import _lib
+
+HEADER = os.path.join(ROOT, "include", "diffpose_kernels.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dpk_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exists():
+    assert os.path.exists(_lib.LIB_PATH), "run `python __graft_entry__.py` (build) first"
+
+
+def test_exports_match_header():
+    decl = declared_functions()
+    assert set(decl) == set(_lib.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    syms = set(re.findall(r"\bT (dpk_\w+)", out))
+    missing = [d for d in decl if d not in syms]
+    assert not missing, f"not exported: {missing}"
+
+
+def test_load_and_query_without_gpu():
+    L = _lib.lib()
+    assert L.dpk_version() >= 100
+    g = _lib.kernel_geometry()
+    assert g["poses_per_workgroup"] >= 1 and g["threads_per_workgroup"] % 64 == 0
+    assert 0 < g["lds_bytes"] <= 160 * 1024
+
+
+def test_argument_validation_without_gpu():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.dpk_create(None, ctypes.byref(h)) == -1
+    bad = _lib.DpkConfig(128, 5, 4, 17, 5, 5, 0)            # hid_dim other than the compiled 96
+    assert L.dpk_create(ctypes.byref(bad), ctypes.byref(h)) == -2
+    assert L.dpk_eps(None, None, None, None, 0, None) == -1
+    assert L.dpk_last_error(None) == b"null handle"
+
+
+def test_no_oracle_in_product_path():
+    pkg = os.path.join(ROOT, "diffpose-nw_amd")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", txt).replace("no oracle", ""), f
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_lib, "_LIB", None)
+    with pytest.raises(ImportError):
+        _lib.lib()
