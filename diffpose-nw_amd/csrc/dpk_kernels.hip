@@ -663,8 +663,26 @@ struct dpk_handle {
     float eta = 0.f;
     unsigned mask = (1u << J) - 1u;
     std::vector<float> h_adj;
-    std::vector<float> a_hat[NL];  // for the GraphNet Laplacians
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
 };
+
+// event pair around a sampler-kernel launch (dpk_profile)
+static int prof_begin(dpk_handle* h, hipStream_t st, std::pair<hipEvent_t, hipEvent_t>& ev) {
+    if (h->ev_free.empty()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return DPK_E_HIP;
+        h->ev_free.push_back({a, b});
+    }
+    ev = h->ev_free.back();
+    h->ev_free.pop_back();
+    return hipEventRecord(ev.first, st) == hipSuccess ? DPK_OK : DPK_E_HIP;
+}
+static int prof_end(dpk_handle* h, hipStream_t st, std::pair<hipEvent_t, hipEvent_t>& ev) {
+    if (hipEventRecord(ev.second, st) != hipSuccess) return DPK_E_HIP;
+    h->ev_used.push_back(ev);
+    return DPK_OK;
+}
 
 static int fail(dpk_handle* h, int code, const std::string& msg) {
     if (h) h->err = msg;
@@ -762,11 +780,16 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
 
 void dpk_destroy(dpk_handle* h) {
     if (!h) return;
-    hipSetDevice(h->device);
-    if (h->arena) hipFree(h->arena);
-    if (h->temb) hipFree(h->temb);
-    if (h->coef) hipFree(h->coef);
-    if (h->tproj) hipFree(h->tproj);
+    (void)hipSetDevice(h->device);
+    if (h->arena) (void)hipFree(h->arena);
+    if (h->temb) (void)hipFree(h->temb);
+    if (h->coef) (void)hipFree(h->coef);
+    if (h->tproj) (void)hipFree(h->tproj);
+    for (auto* v : {&h->ev_used, &h->ev_free})
+        for (auto& e : *v) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
     delete h;
 }
 
@@ -987,8 +1010,11 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     a.N = N;
     a.K = 1;
     a.mask = h->mask;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     hipLaunchKernelGGL(sample_kernel<true>, dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
+    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
 }
 
@@ -1020,8 +1046,34 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.mask = h->mask;
     a.eta = h->eta;
     a.seed = seed;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     hipLaunchKernelGGL(sample_kernel<false>, dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
+    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
+    return DPK_OK;
+}
+
+int dpk_profile(dpk_handle* h, int enable) {
+    if (!h) return DPK_E_INVALID;
+    h->profiling = enable != 0;
+    return DPK_OK;
+}
+
+int dpk_profile_read(dpk_handle* h, float* ms, int cap, int* count) {
+    if (!h || (cap > 0 && !ms)) return fail(h, DPK_E_INVALID, "dpk_profile_read: bad args");
+    HIPCHK(h, hipSetDevice(h->device));
+    int n = 0;
+    for (auto& e : h->ev_used) {
+        HIPCHK(h, hipEventSynchronize(e.second));
+        float t = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&t, e.first, e.second));
+        if (n < cap) ms[n] = t;
+        ++n;
+        h->ev_free.push_back(e);
+    }
+    h->ev_used.clear();
+    if (count) *count = n;
     return DPK_OK;
 }
 

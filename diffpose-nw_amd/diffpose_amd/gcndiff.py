@@ -211,6 +211,19 @@ class HipGCNdiff:
         _lib.check(self._h, "dpk_ddim_update", rc)
         return xn, x0
 
+    def profile(self, enable: bool = True) -> None:
+        """Bracket each sampler-kernel launch with HIP events (see dpk_profile)."""
+        _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))
+
+    def kernel_times_ms(self):
+        """Wait for and return the recorded sampler-kernel durations (ms), oldest first."""
+        L = _lib.lib()
+        cap = 4096
+        buf = (ctypes.c_float * cap)()
+        n = ctypes.c_int()
+        _lib.check(self._h, "dpk_profile_read", L.dpk_profile_read(self._h, buf, cap, ctypes.byref(n)))
+        return [buf[i] for i in range(min(n.value, cap))]
+
     def close(self):
         h, self._h = getattr(self, "_h", None), None
         if h:

@@ -100,6 +100,13 @@ int dpk_sample(dpk_handle* h, const float* x_dev, float* out_dev, float* xs_dev,
 int dpk_ddim_update(dpk_handle* h, const float* xt_dev, const float* eps_dev, float* xnext_dev,
                     float* x0_dev, int64_t n_elems, int step, uint64_t seed, void* stream);
 
+/* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /
+ * dpk_eps brackets its sampler-kernel launch with a pair of HIP events on the
+ * caller's stream.  dpk_profile_read waits for the recorded events and returns up to
+ * `cap` elapsed times in ms (oldest first), then clears them. */
+int dpk_profile(dpk_handle* h, int enable);
+int dpk_profile_read(dpk_handle* h, float* ms_out, int cap, int* count);
+
 /* Poses per workgroup of the sampler kernel and its static LDS bytes (for docs/bench). */
 int dpk_kernel_geometry(int* poses_per_workgroup, int* threads_per_workgroup, int* lds_bytes);
 
