@@ -24,6 +24,16 @@
 
 #include "diffpose_kernels.h"
 
+// Timing-only ablation builds (tools/ablate.py): bit set = phase skipped.  Outputs of such
+// a build are wrong by construction; the shipped library is built with DPK_ABLATE=0.
+#ifndef DPK_ABLATE
+#define DPK_ABLATE 0
+#endif
+#define DPK_RUN(bit) ((DPK_ABLATE & (bit)) == 0)
+#ifndef DPK_EXP
+#define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
+#endif
+
 namespace dpk {
 
 // ---------------------------------------------------------------------------------------
@@ -53,10 +63,7 @@ constexpr int SM_XS = 0;                    // residual stream   [R][LDX]
 constexpr int SM_B1 = SM_XS + R * LDX;      // 96-wide scratch   [R][LDX]
 constexpr int SM_B2 = SM_B1 + R * LDX;      // 288-wide scratch  [R][LD2]
 constexpr int SM_XST = SM_B2 + R * LD2;     // pose state x_t    [R][5]
-constexpr int SM_T1 = SM_XST + ((R * CIN + 3) / 4) * 4;
-constexpr int SM_T2 = SM_T1 + 292;
-constexpr int SM_LG = SM_T2 + 292;          // 5 GraphNet Laplacians [NL][17][17]
-constexpr int SM_FLOATS = SM_LG + ((NL * J * J + 3) / 4) * 4;
+constexpr int SM_FLOATS = SM_XST + ((R * CIN + 3) / 4) * 4;
 static_assert(SM_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
 // packed-weight blocks: one block = 16 cols x 16 k = 64 lanes x float4
@@ -85,9 +92,9 @@ constexpr int OFF_WIN = NL * LAYER_FLOATS;                  // [6 ct][1 kb]  (K=
 constexpr int OFF_WOUT = OFF_WIN + 6 * 1 * BLK;             // [1 ct][18 kb] (N=5 padded to 16)
 constexpr int OFF_BIN = OFF_WOUT + 1 * KB_D3 * BLK;
 constexpr int OFF_BOUT = OFF_BIN + D;                       // 16 (5 used)
-constexpr int OFF_T1 = OFF_BOUT + 16;                       // 17x17 dense Chebyshev T1
-constexpr int OFF_T2 = OFF_T1 + 292;
-constexpr int ARENA_FLOATS = ((OFF_T2 + 292 + 63) / 64) * 64;
+constexpr int OFF_CHEB = OFF_BOUT + 16;                     // dense T1 [17x17] then T2 [17x17]
+constexpr int OFF_CHEBS = OFF_CHEB + 2 * J * J;             // H36M-sparse T1 (49) then T2 (87) values
+constexpr int ARENA_FLOATS = ((OFF_CHEBS + 136 + 63) / 64) * 64;
 
 // timestep-MLP arena (transposed nn.Linear weights: [in][out])
 constexpr int TOFF_W0 = 0;                    // [96][384]
@@ -164,178 +171,298 @@ __device__ __forceinline__ int opaque(int x) {
 // A: LDS rows (k in [0,16*KB0) from A0, [16*KB0, 16*(KB0+KB1)) from A1); B: packed blocks.
 // Lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for MFMA sub-step j, and the
 // packed B block holds W[k = same][n = ct*16 + (l&15)]: a consistent permutation of k.
-template <int NR, int NCW, int KB0, int KB1, class Epi>
-__device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float* A1, int lda1,
-                                          const f32x4* __restrict__ Bp, int rt0, int ct0, int lane, Epi epi) {
-    constexpr int KB = KB0 + KB1;
-    lane = opaque(lane);
+// rt0/ct0 are wave-uniform (SGPR): B addresses are scalar base + lane*16.  The k-loop is a
+// 2-stage register ring (named buffers, unrolled by 2): the B (global/L2) and A (LDS)
+// fragments of k-block kb+1 are in flight while the MFMAs of kb issue.
+template <int NR, int NCW, int KB0, int KB1>
+struct GemmTile {
+    static constexpr int KB = KB0 + KB1;
     f32x4 acc[NR][NCW];
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-        for (int c = 0; c < NCW; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int aoff0[NR], aoff1[NR];
 
-    const int rl = lane & 15, kq = (lane >> 4) * 4;
-    int row[NR];
+    __device__ __forceinline__ void load(f32x4 (&a)[NR], f32x4 (&b)[NCW], const float* A0, const float* A1,
+                                         const f32x4* __restrict__ Bl, int kb) const {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int r = (rt0 + i) * 16 + rl;
-        row[i] = r < R ? r : R - 1;     // clamp padding rows (outputs discarded)
-    }
-    f32x4 bcur[NCW];
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) bcur[c] = Bp[((ct0 + c) * KB + 0) * 64 + lane];
-
-#pragma unroll 1
-    for (int kb = 0; kb < KB; ++kb) {
-        f32x4 bnext[NCW];
-        if (kb + 1 < KB) {
-#pragma unroll
-            for (int c = 0; c < NCW; ++c) bnext[c] = Bp[((ct0 + c) * KB + kb + 1) * 64 + lane];
-        }
-        f32x4 a[NR];
+        for (int c = 0; c < NCW; ++c) b[c] = Bl[(c * KB + kb) * 64];
         if (kb < KB0) {
 #pragma unroll
-            for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A0 + row[i] * lda0 + kb * 16 + kq);
+            for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A0 + aoff0[i] + kb * 16);
         } else {
 #pragma unroll
-            for (int i = 0; i < NR; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(A1 + row[i] * lda1 + (kb - KB0) * 16 + kq);
+            for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A1 + aoff1[i] + (kb - KB0) * 16);
         }
+    }
+    __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&b)[NCW]) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int i = 0; i < NR; ++i)
 #pragma unroll
                 for (int c = 0; c < NCW; ++c)
-                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], bcur[c][j], acc[i][c], 0, 0, 0);
-        if (kb + 1 < KB) {
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+    }
+};
+
+// Epilogue modes (out = acc + bias[col]):
+//   E_STORE       dst = out                       (QKV, gconv_input)
+//   E_STORE_RELU  dst = relu(out)                 (GraphNet fc1)
+//   E_RESID       dst = dst + out                 (attention O-proj, GraphNet fc2)
+//   E_RESID_RELU  dst = dst + relu(out)           (Cheb2 of _ResChebGC_diff)
+//   E_CHEB1       dst = relu(out) + tproj[col]    (Cheb1 + temb_proj injection)
+//   E_STORE_NB    dst = acc (no bias)             (GraphNet fc2 before its graph product)
+// Bias / temb columns are loaded into registers before the k-loop and residual values are
+// read in one batch, so the epilogue is LDS + VALU only (no per-element global round trip).
+enum { E_STORE = 0, E_STORE_RELU, E_RESID, E_RESID_RELU, E_CHEB1, E_STORE_NB };
+
+struct EpiArgs {
+    float* dst;
+    int ldd;
+    const float* bias;
+    const float* tproj;     // E_CHEB1: temb_proj row (sample mode) or per-pose base (eps mode)
+    int tproj_pose_stride;  // 0: one row for all poses; else floats between consecutive poses
+    int pose0;              // global index of the workgroup's first pose (eps mode clamp)
+    int pose_max;           // N-1
+};
+
+template <int NR, int NCW, int KB0, int KB1, int MODE, bool PARTIAL>
+__device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float* A1, int lda1,
+                                          const f32x4* __restrict__ Bp, int rt0, int ct0, int lane,
+                                          const EpiArgs& e) {
+    using T = GemmTile<NR, NCW, KB0, KB1>;
+    constexpr int KB = T::KB;
+    lane = opaque(lane);
+    T g;
 #pragma unroll
-            for (int c = 0; c < NCW; ++c) bcur[c] = bnext[c];
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int c = 0; c < NCW; ++c) g.acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = lane & 15, kq = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        int r = (rt0 + i) * 16 + rl;
+        r = r < R ? r : R - 1;          // clamp padding rows (outputs discarded)
+        g.aoff0[i] = r * lda0 + kq;
+        g.aoff1[i] = r * lda1 + kq;
+    }
+    float bcol[NCW], tcol[NCW];
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+        bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[(ct0 + c) * 16 + rl];
+        tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[(ct0 + c) * 16 + rl] : 0.f;
+    }
+    const f32x4* Bl = Bp + (size_t)ct0 * KB * 64 + lane;
+    f32x4 a0[NR], b0[NCW];
+    g.load(a0, b0, A0, A1, Bl, 0);
+    if constexpr (KB == 1) {
+        g.mma(a0, b0);
+    } else {
+        static_assert(KB % 2 == 0, "k-blocks in pairs");
+        f32x4 a1[NR], b1[NCW];
+#pragma unroll 1
+        for (int kb = 0; kb < KB; kb += 2) {
+            g.load(a1, b1, A0, A1, Bl, kb + 1);
+            g.mma(a0, b0);
+            if (kb + 2 < KB) g.load(a0, b0, A0, A1, Bl, kb + 2);
+            g.mma(a1, b1);
         }
     }
-    // C/D map of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + r
+    if (DPK_EXP & 1) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < NCW; ++c) asm volatile("" ::"v"(g.acc[i][c]));
+        return;
+    }
+    // C/D map of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + r.  The partial tile (rows
+    // 64..79 of which 64..67 exist) keeps lanes 0-15 only.
+    if (PARTIAL && kq != 0) return;
+    float* d = e.dst + ((rt0 * 16 + kq) * e.ldd + ct0 * 16 + rl);
+    float old[NR][NCW][4];
+    if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < NCW; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + c * 16];
+    }
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
         for (int c = 0; c < NCW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int orow = (rt0 + i) * 16 + kq + r;
-                if (orow < R) epi(orow, (ct0 + c) * 16 + rl, acc[i][c][r]);
+                const float v = g.acc[i][c][r] + bcol[c];
+                float o;
+                if constexpr (MODE == E_STORE_NB) o = g.acc[i][c][r];
+                else if constexpr (MODE == E_STORE) o = v;
+                else if constexpr (MODE == E_STORE_RELU) o = fmaxf(v, 0.f);
+                else if constexpr (MODE == E_RESID) o = old[i][c][r] + v;
+                else if constexpr (MODE == E_RESID_RELU) o = old[i][c][r] + fmaxf(v, 0.f);
+                else {
+                    float tp = tcol[c];
+                    if (e.tproj_pose_stride != 0) {
+                        const int pose = min(e.pose0 + ((rt0 + i) * 16 + kq + r) / J, e.pose_max);
+                        tp = e.tproj[(size_t)pose * e.tproj_pose_stride + (ct0 + c) * 16 + rl];
+                    }
+                    o = fmaxf(v, 0.f) + tp;
+                }
+                d[(i * 16 + r) * e.ldd + c * 16] = o;
             }
 }
 
-// Whole-workgroup GEMM with NC (multiple of 3) output col tiles.
-template <int NC, int KB0, int KB1, class Epi>
+// Whole-workgroup GEMM with NC (multiple of 3) output col tiles.  `wave` must be uniform.
+template <int NC, int KB0, int KB1, int MODE>
 __device__ __forceinline__ void gemm_wg(const float* A0, int lda0, const float* A1, int lda1, const float* Bp,
-                                        int wave, int lane, Epi epi) {
+                                        int wave, int lane, const EpiArgs& e) {
     static_assert(NC % 3 == 0, "column tiles split in thirds");
     const f32x4* B = reinterpret_cast<const f32x4*>(Bp);
     if (wave < 3) {
-        gemm_wave<4, NC / 3, KB0, KB1>(A0, lda0, A1, lda1, B, 0, wave * (NC / 3), lane, epi);
-    } else {
-        // wave 3: the partial row tile across all columns, in passes of <= 6 column tiles
-        constexpr int CH = NC < 6 ? NC : 6;
+        gemm_wave<4, NC / 3, KB0, KB1, MODE, false>(A0, lda0, A1, lda1, B, 0, wave * (NC / 3), lane, e);
+    } else if (!(DPK_EXP & 2)) {
+        // wave 3: the partial row tile across all columns, in passes of <= 12 column tiles
+        constexpr int CH = NC <= 12 ? NC : NC / 2;
         static_assert(NC % CH == 0, "column chunking");
 #pragma unroll 1
-        for (int c0 = 0; c0 < NC; c0 += CH) gemm_wave<1, CH, KB0, KB1>(A0, lda0, A1, lda1, B, 4, c0, lane, epi);
+        for (int c0 = 0; c0 < NC; c0 += CH)
+            gemm_wave<1, CH, KB0, KB1, MODE, true>(A0, lda0, A1, lda1, B, 4, c0, lane, e);
     }
 }
 
+// Output ChebConv (96->5, one col tile): raw accumulators handed to a functor (DDIM update).
+template <int NR, int KB0, int KB1, class Epi>
+__device__ __forceinline__ void gemm_out(const float* A0, int lda0, const float* A1, int lda1,
+                                         const f32x4* __restrict__ Bp, int rt0, int lane, Epi epi) {
+    using T = GemmTile<NR, 1, KB0, KB1>;
+    constexpr int KB = T::KB;
+    lane = opaque(lane);
+    T g;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) g.acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = lane & 15, kq = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        int r = (rt0 + i) * 16 + rl;
+        r = r < R ? r : R - 1;
+        g.aoff0[i] = r * lda0 + kq;
+        g.aoff1[i] = r * lda1 + kq;
+    }
+    const f32x4* Bl = Bp + lane;
+    f32x4 a0[NR], b0[1], a1[NR], b1[1];
+    g.load(a0, b0, A0, A1, Bl, 0);
+#pragma unroll 1
+    for (int kb = 0; kb < KB; kb += 2) {
+        g.load(a1, b1, A0, A1, Bl, kb + 1);
+        g.mma(a0, b0);
+        if (kb + 2 < KB) g.load(a0, b0, A0, A1, Bl, kb + 2);
+        g.mma(a1, b1);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int orow = (rt0 + i) * 16 + kq + r;
+            if (orow < R && rl < COUT) epi(orow, rl, g.acc[i][0][r]);
+        }
+}
+
 // ---------------------------------------------------------------------------------------
-// LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b.
-// 16 lanes per row, 6 features per lane; mean/var accumulated in double.
+// Correctly rounded x / d from a shared reciprocal r = 1/d (Markstein: one fma residual
+// correction).  Used where a whole row is divided by one value (LayerNorm).
+__device__ __forceinline__ float div_by(float x, float d, float r) {
+    const float q = x * r;
+    const float e = fmaf(-q, d, x);
+    return fmaf(e, r, q);
+}
+
+// LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b, one pass:
+// 3 lanes per row (32 features each), 21 rows per wave; mean/var accumulated in double.
 __device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* __restrict__ gain,
                                            const float* __restrict__ shift, int tid) {
     tid = opaque(tid);
-    const int w = tid >> 6, lane = tid & 63, sub = lane >> 4, q = lane & 15;
-    float g[6], b[6];
+    const int w = tid >> 6, lane = tid & 63;
+    const int row = w * 21 + lane / 3, part = lane % 3;
+    const bool ok = lane < 63 && row < R;
+    const int rr = ok ? row : R - 1;
+    const float* s = src + rr * LDX + 32 * part;
+    float v[32];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) {
-        g[e] = gain[6 * q + e];
-        b[e] = shift[6 * q + e];
+    for (int e = 0; e < 32; e += 4) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(s + e);
+        v[e] = t[0]; v[e + 1] = t[1]; v[e + 2] = t[2]; v[e + 3] = t[3];
     }
-#pragma unroll 1
-    for (int it = 0; it < 5; ++it) {
-        const int row = it * 16 + w * 4 + sub;
-        const int rr = row < R ? row : R - 1;
-        const float* s = src + rr * LDX + 6 * q;
-        float v[6];
+    const int base = (lane / 3) * 3;
+    double sum = 0.0;
 #pragma unroll
-        for (int e = 0; e < 6; e += 2) {
-            const float2 t = *reinterpret_cast<const float2*>(s + e);
-            v[e] = t.x;
-            v[e + 1] = t.y;
+    for (int e = 0; e < 32; ++e) sum += (double)v[e];
+    // identical combination order in the three lanes of a row
+    const double s0 = __shfl(sum, base, 64), s1 = __shfl(sum, base + 1, 64), s2 = __shfl(sum, base + 2, 64);
+    const double mean_d = ((s0 + s1) + s2) / (double)D;
+    double ss = 0.0;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+        const double dv = (double)v[e] - mean_d;
+        ss += dv * dv;
+    }
+    const double q0 = __shfl(ss, base, 64), q1 = __shfl(ss, base + 1, 64), q2 = __shfl(ss, base + 2, 64);
+    const float mean = (float)mean_d;
+    const float den = (float)sqrt(((q0 + q1) + q2) / (double)(D - 1)) + LN_EPS;
+    const float rcp = 1.0f / den;
+    if (!ok) return;
+    float* d = dst + row * LDX + 32 * part;
+#pragma unroll
+    for (int e = 0; e < 32; e += 4) {
+        f32x4 t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = 32 * part + e + k;
+            t[k] = div_by(gain[c] * (v[e + k] - mean), den, rcp) + shift[c];
         }
-        double sum = 0.0;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) sum += (double)v[e];
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
-        const double mean_d = sum / (double)D;
-        double ss = 0.0;
-#pragma unroll
-        for (int e = 0; e < 6; ++e) {
-            const double dv = (double)v[e] - mean_d;
-            ss += dv * dv;
-        }
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 16);
-        const float mean = (float)mean_d;
-        const float den = (float)sqrt(ss / (double)(D - 1)) + LN_EPS;
-        if (row < R) {
-            float* d = dst + row * LDX + 6 * q;
-#pragma unroll
-            for (int e = 0; e < 6; e += 2) {
-                float2 t;
-                t.x = (g[e] * (v[e] - mean)) / den + b[e];
-                t.y = (g[e + 1] * (v[e + 1] - mean)) / den + b[e + 1];
-                *reinterpret_cast<float2*>(d + e) = t;
-            }
-        }
+        *reinterpret_cast<f32x4*>(d + e) = t;
     }
 }
 
 // 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
-// projections).  One thread per (pose, head, query); scores/softmax/PV in registers.
+// projections).  16 lanes per (pose, head): lane q owns query q (scores, softmax and PV in
+// registers); query 16 is computed cooperatively by the 16 lanes (one key each, group
+// reductions by shuffles).
 __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
     tid = opaque(tid);
-#pragma unroll 1
-    for (int item = tid; item < P * NH * J; item += NT) {
-        const int p = item / (NH * J);
-        const int rem = item - p * (NH * J);
-        const int h = rem / J;
-        const int i = rem - h * J;
-        const float* qr = qkv + (p * J + i) * LD2 + h * DK;
-        float q[DK];
+    const int grp = tid >> 4, q = tid & 15;
+    const int p = grp >> 2, h = grp & 3;
+    const float* rows = qkv + p * J * LD2 + h * DK;     // row i: + i*LD2; K at +D, V at +2D
+    float* orows = out + p * J * LDX + h * DK;
+    auto keyok = [&](int j) { return ((mask >> j) & 1u) != 0u; };
+    // ---- query q
+    {
+        float qv[DK];
 #pragma unroll
         for (int d = 0; d < DK; d += 4) {
-            const f32x4 t = *reinterpret_cast<const f32x4*>(qr + d);
-            q[d] = t[0]; q[d + 1] = t[1]; q[d + 2] = t[2]; q[d + 3] = t[3];
+            const f32x4 t = *reinterpret_cast<const f32x4*>(rows + q * LD2 + d);
+            qv[d] = t[0]; qv[d + 1] = t[1]; qv[d + 2] = t[2]; qv[d + 3] = t[3];
         }
-        float s[J];
+        float sc[J];
         float m = -INFINITY;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const float* kr = qkv + (p * J + j) * LD2 + D + h * DK;
+            const float* kr = rows + j * LD2 + D;
             float dot = 0.f;
 #pragma unroll
             for (int d = 0; d < DK; d += 4) {
                 const f32x4 t = *reinterpret_cast<const f32x4*>(kr + d);
-                dot = fmaf(q[d], t[0], dot);
-                dot = fmaf(q[d + 1], t[1], dot);
-                dot = fmaf(q[d + 2], t[2], dot);
-                dot = fmaf(q[d + 3], t[3], dot);
+                dot = fmaf(qv[d], t[0], dot);
+                dot = fmaf(qv[d + 1], t[1], dot);
+                dot = fmaf(qv[d + 2], t[2], dot);
+                dot = fmaf(qv[d + 3], t[3], dot);
             }
-            s[j] = ((mask >> j) & 1u) ? dot / SQRT_DK : -1e9f;
-            m = fmaxf(m, s[j]);
+            sc[j] = keyok(j) ? dot / SQRT_DK : -1e9f;
+            m = fmaxf(m, sc[j]);
         }
         float sum = 0.f;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            s[j] = expf(s[j] - m);
-            sum += s[j];
+            sc[j] = expf(sc[j] - m);
+            sum += sc[j];
         }
         const float inv = 1.0f / sum;
         float o[DK];
@@ -343,8 +470,8 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
         for (int d = 0; d < DK; ++d) o[d] = 0.f;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const float pj = s[j] * inv;
-            const float* vr = qkv + (p * J + j) * LD2 + 2 * D + h * DK;
+            const float pj = sc[j] * inv;
+            const float* vr = rows + j * LD2 + 2 * D;
 #pragma unroll
             for (int d = 0; d < DK; d += 4) {
                 const f32x4 t = *reinterpret_cast<const f32x4*>(vr + d);
@@ -354,211 +481,320 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
                 o[d + 3] = fmaf(pj, t[3], o[d + 3]);
             }
         }
-        float* orow = out + (p * J + i) * LDX + h * DK;
 #pragma unroll
-        for (int d = 0; d < DK; d += 4) *reinterpret_cast<f32x4*>(orow + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+        for (int d = 0; d < DK; d += 4)
+            *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+    }
+    // ---- query 16: lane q scores key q (lane 0 also key 16)
+    {
+        const float* q16 = rows + 16 * LD2;
+        auto score = [&](int j) {
+            const float* kr = rows + j * LD2 + D;
+            float dot = 0.f;
+#pragma unroll
+            for (int d = 0; d < DK; d += 4) {
+                const f32x4 a4 = *reinterpret_cast<const f32x4*>(q16 + d);
+                const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + d);
+                dot = fmaf(a4[0], k4[0], dot);
+                dot = fmaf(a4[1], k4[1], dot);
+                dot = fmaf(a4[2], k4[2], dot);
+                dot = fmaf(a4[3], k4[3], dot);
+            }
+            return keyok(j) ? dot / SQRT_DK : -1e9f;
+        };
+        const float sq = score(q);
+        const float s16 = __shfl(score(16), 0, 16);        // every lane computes it; broadcast lane 0's
+        float m = fmaxf(sq, s16);
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+        const float eq = expf(sq - m), e16 = expf(s16 - m);
+        float sum = eq;
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
+        sum += e16;
+        const float inv = 1.0f / sum;
+        const float pq = eq * inv, p16 = e16 * inv;
+        // output dims d = q and d = q + 16 (q < 8): o_d = sum_j P_j V[j][d]
+        float o0 = 0.f, o1 = 0.f;
+        const float* vcol = rows + 2 * D;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float pj = __shfl(pq, j, 16);
+            o0 = fmaf(pj, vcol[j * LD2 + q], o0);
+            if (q < 8) o1 = fmaf(pj, vcol[j * LD2 + q + 16], o1);
+        }
+        o0 = fmaf(p16, vcol[16 * LD2 + q], o0);
+        orows[16 * LDX + q] = o0;
+        if (q < 8) {
+            o1 = fmaf(p16, vcol[16 * LD2 + q + 16], o1);
+            orows[16 * LDX + q + 16] = o1;
+        }
     }
 }
 
-// dst[:, c] = M @ src[:, c] per pose (17x17 M in LDS), G columns per thread; in-place safe.
-template <int G>
-__device__ __forceinline__ void graph_apply(const float* M, const float* src, int lds, float* dst, int ldd,
-                                            int ncols, int tid) {
-    tid = opaque(tid);
-    const int ng = ncols / G;      // P*ng <= NT: one item per thread, no loop (keeps M out of registers)
-    {
-        const int item = tid;
-        if (item >= P * ng) return;
-        const int p = item / ng;
-        const int c = (item - p * ng) * G;
-        float v[J][G];
-#pragma unroll
-        for (int i = 0; i < J; ++i)
-#pragma unroll
-            for (int g = 0; g < G; ++g) v[i][g] = src[(p * J + i) * lds + c + g];
-        float o[J][G];
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float a = 0.f;
-#pragma unroll
-                for (int i = 0; i < J; ++i) a = fmaf(M[j * J + i], v[i][g], a);
-                o[j][g] = a;
-            }
-#pragma unroll
-        for (int j = 0; j < J; ++j)
-#pragma unroll
-            for (int g = 0; g < G; ++g) dst[(p * J + j) * ldd + c + g] = o[j][g];
+// --- graph products -------------------------------------------------------------------
+// Chebyshev terms T1 = L, T2 = 2L^2 - I of the H36M skeleton (runners/diffpose_frame.py:120-124)
+// are sparse (49 / 87 of 289 entries).  Their pattern is derived here at compile time from the
+// edge list; dpk_set_graph() checks a given adjacency against it and packs the nonzero values
+// (row-major over the pattern) — any other graph runs the dense path.
+constexpr int H36M_EDGES[16][2] = {{0, 1}, {1, 2}, {2, 3}, {0, 4}, {4, 5}, {5, 6}, {0, 7}, {7, 8},
+                                   {8, 9}, {9, 10}, {8, 11}, {11, 12}, {12, 13}, {8, 14}, {14, 15}, {15, 16}};
+struct SparsePattern {
+    int n1[J], c1[J][J], o1[J];
+    int n2[J], c2[J][J], o2[J];
+    int nnz1, nnz2;
+};
+constexpr SparsePattern make_pattern() {
+    SparsePattern sp{};
+    bool a[J][J] = {};
+    for (int i = 0; i < J; ++i) a[i][i] = true;
+    for (int e = 0; e < 16; ++e) {
+        a[H36M_EDGES[e][0]][H36M_EDGES[e][1]] = true;
+        a[H36M_EDGES[e][1]][H36M_EDGES[e][0]] = true;
     }
+    int t1 = 0, t2 = 0;
+    for (int i = 0; i < J; ++i) {
+        sp.n1[i] = 0;
+        sp.n2[i] = 0;
+        sp.o1[i] = t1;
+        sp.o2[i] = t2;
+        for (int j = 0; j < J; ++j) {
+            bool two = false;
+            for (int k = 0; k < J; ++k) two = two || (a[i][k] && a[k][j]);
+            if (a[i][j]) sp.c1[i][sp.n1[i]++] = j;
+            if (two) sp.c2[i][sp.n2[i]++] = j;
+        }
+        t1 += sp.n1[i];
+        t2 += sp.n2[i];
+    }
+    sp.nnz1 = t1;
+    sp.nnz2 = t2;
+    return sp;
 }
+constexpr SparsePattern SPAT = make_pattern();
+static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 
 // Chebyshev prologue: B2[:, 0:96] = T1 src, B2[:, 96:192] = T2 src (ChebConv.py:83).
-__device__ __forceinline__ void cheb_prep(const float* T1, const float* T2, const float* src, float* b2, int tid) {
+// One thread per (pose, column pair).  SPARSE: compile-time pattern, packed values (scalar
+// loads); dense: 17x17 from the arena.  Sums run over increasing i in both (identical bits).
+template <bool SPARSE>
+__device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int tid) {
     tid = opaque(tid);
     constexpr int G = 2, ng = D / G;
     static_assert(P * ng <= NT, "one item per thread");
-    {
-        const int item = tid;
-        if (item >= P * ng) return;
-        const int p = item / ng;
-        const int c = (item - p * ng) * G;
-        float v[J][G];
+    if (tid >= P * ng) return;
+    const int p = tid / ng;
+    const int c = (tid - p * ng) * G;
+    float v[J][G];
 #pragma unroll
-        for (int i = 0; i < J; ++i) {
-            const float2 t = *reinterpret_cast<const float2*>(src + (p * J + i) * LDX + c);
-            v[i][0] = t.x;
-            v[i][1] = t.y;
-        }
+    for (int i = 0; i < J; ++i) {
+        const float2 t = *reinterpret_cast<const float2*>(src + (p * J + i) * LDX + c);
+        v[i][0] = t.x;
+        v[i][1] = t.y;
+    }
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
+    for (int j = 0; j < J; ++j) {
+        float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
+        if constexpr (SPARSE) {
+#pragma unroll
+            for (int k = 0; k < SPAT.n1[j]; ++k) {
+                const float w = cw[SPAT.o1[j] + k];
+                a0 = fmaf(w, v[SPAT.c1[j][k]][0], a0);
+                a1 = fmaf(w, v[SPAT.c1[j][k]][1], a1);
+            }
+#pragma unroll
+            for (int k = 0; k < SPAT.n2[j]; ++k) {
+                const float w = cw[SPAT.nnz1 + SPAT.o2[j] + k];
+                c0 = fmaf(w, v[SPAT.c2[j][k]][0], c0);
+                c1 = fmaf(w, v[SPAT.c2[j][k]][1], c1);
+            }
+        } else {
 #pragma unroll
             for (int i = 0; i < J; ++i) {
-                const float t1 = T1[j * J + i], t2 = T2[j * J + i];
+                const float t1 = cw[j * J + i], t2 = cw[J * J + j * J + i];
                 a0 = fmaf(t1, v[i][0], a0);
                 a1 = fmaf(t1, v[i][1], a1);
                 c0 = fmaf(t2, v[i][0], c0);
                 c1 = fmaf(t2, v[i][1], c1);
             }
-            *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + c) = make_float2(a0, a1);
-            *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + D + c) = make_float2(c0, c1);
+        }
+        *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + c) = make_float2(a0, a1);
+        *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + D + c) = make_float2(c0, c1);
+    }
+}
+
+// GraphNet products with the layer's dense 17x17 Laplacian L (GraFormer.py:174-183), L read
+// with uniform (scalar) loads.  One thread per (pose, column pair); in place.
+//   graph_apply:  buf[:, c] = L @ buf[:, c]
+//   graph_resid:  xs[:, c] += L @ y[:, c] + bias[c]   (fc2 reordered: L (X1 W2^T) + b2)
+template <bool RESID>
+__device__ __forceinline__ void graph_op(const float* __restrict__ L, const float* src, float* dst,
+                                         const float* __restrict__ bias, int tid) {
+    tid = opaque(tid);
+    constexpr int G = 2, ng = D / G;
+    if (tid >= P * ng) return;
+    const int p = tid / ng;
+    const int c = (tid - p * ng) * G;
+    float v[J][G];
+#pragma unroll
+    for (int i = 0; i < J; ++i) {
+        const float2 t = *reinterpret_cast<const float2*>(src + (p * J + i) * LDX + c);
+        v[i][0] = t.x;
+        v[i][1] = t.y;
+    }
+    float b0 = 0.f, b1 = 0.f;
+    if (RESID) {
+        b0 = bias[c];
+        b1 = bias[c + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < J; ++i) {
+            const float w = L[j * J + i];
+            a0 = fmaf(w, v[i][0], a0);
+            a1 = fmaf(w, v[i][1], a1);
+        }
+        float2* o = reinterpret_cast<float2*>(dst + (p * J + j) * LDX + c);
+        if (RESID) {
+            const float2 x = *o;
+            *o = make_float2(x.x + (a0 + b0), x.y + (a1 + b1));
+        } else {
+            *o = make_float2(a0, a1);
         }
     }
 }
 
 // ---------------------------------------------------------------------------------------
+// gconv_input prologue: B1[:, 0:16] = [x | T1 x | T2 x | 0] for the 5 pose channels.
+template <bool SPARSE>
+__device__ __forceinline__ void input_prep(const float* __restrict__ cw, const float* xst, float* b1, int tid) {
+    tid = opaque(tid);
+    if (tid >= P * CIN) return;
+    const int p = tid / CIN, c = tid - p * CIN;
+    float v[J];
+#pragma unroll
+    for (int i = 0; i < J; ++i) v[i] = xst[(p * J + i) * CIN + c];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        float a1 = 0.f, a2 = 0.f;
+        if constexpr (SPARSE) {
+#pragma unroll
+            for (int k = 0; k < SPAT.n1[j]; ++k) a1 = fmaf(cw[SPAT.o1[j] + k], v[SPAT.c1[j][k]], a1);
+#pragma unroll
+            for (int k = 0; k < SPAT.n2[j]; ++k) a2 = fmaf(cw[SPAT.nnz1 + SPAT.o2[j] + k], v[SPAT.c2[j][k]], a2);
+        } else {
+#pragma unroll
+            for (int i = 0; i < J; ++i) {
+                a1 = fmaf(cw[j * J + i], v[i], a1);
+                a2 = fmaf(cw[J * J + j * J + i], v[i], a2);
+            }
+        }
+        float* rowp = b1 + (p * J + j) * LDX;
+        rowp[c] = v[j];
+        rowp[CIN + c] = a1;
+        rowp[2 * CIN + c] = a2;
+        if (c == 0) rowp[3 * CIN] = 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // The sampler: K DDIM steps (or one eps evaluation) for P poses per workgroup.
-template <bool EPS_MODE>
+template <bool EPS_MODE, bool SPARSE>
 __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
     float* XS = sm + SM_XS;
     float* B1 = sm + SM_B1;
     float* B2 = sm + SM_B2;
     float* XST = sm + SM_XST;
-    float* T1 = sm + SM_T1;
-    float* T2 = sm + SM_T2;
-    float* LG = sm + SM_LG;
 
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
     const int pose0 = blockIdx.x * P;
     const int npose = min(P, a.N - pose0);
     const int nvalid = npose * PE;
     const float* W = a.arena;
+    const float* CW = W + (SPARSE ? OFF_CHEBS : OFF_CHEB);
 
-    for (int i = tid; i < J * J; i += NT) {
-        T1[i] = W[OFF_T1 + i];
-        T2[i] = W[OFF_T2 + i];
-    }
-    for (int i = tid; i < NL * J * J; i += NT) LG[i] = W[(i / (J * J)) * LAYER_FLOATS + OFF_LG + (i % (J * J))];
     for (int i = tid; i < R * CIN; i += NT) XST[i] = i < nvalid ? a.x_in[(size_t)pose0 * PE + i] : 0.f;
     __syncthreads();
 
     const int K = EPS_MODE ? 1 : a.K;
 #pragma unroll 1
     for (int s = 0; s < K; ++s) {
-        // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108): A = [x | T1 x | T2 x | 0]
-        if (tid < P * CIN) {
-            const int p = tid / CIN, c = tid - p * CIN;
-            float v[J];
-#pragma unroll
-            for (int i = 0; i < J; ++i) v[i] = XST[(p * J + i) * CIN + c];
-#pragma unroll
-            for (int j = 0; j < J; ++j) {
-                float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-                for (int i = 0; i < J; ++i) {
-                    a1 = fmaf(T1[j * J + i], v[i], a1);
-                    a2 = fmaf(T2[j * J + i], v[i], a2);
-                }
-                float* rowp = B1 + (p * J + j) * LDX;
-                rowp[c] = v[j];
-                rowp[CIN + c] = a1;
-                rowp[2 * CIN + c] = a2;
-                if (c == 0) rowp[3 * CIN] = 0.f;
-            }
-        }
+        // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
+        input_prep<SPARSE>(CW, XST, B1, tid);
         __syncthreads();
         {
-            const float* bias = W + OFF_BIN;
-            gemm_wg<6, 1, 0>(B1, LDX, nullptr, 0, W + OFF_WIN, wave, lane,
-                             [&](int r, int c, float v) { XS[r * LDX + c] = v + bias[c]; });
+            const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1};
+            gemm_wg<6, 1, 0, E_STORE>(B1, LDX, nullptr, 0, W + OFF_WIN, wave, lane, e);
         }
         __syncthreads();
 
 #pragma unroll 1
         for (int l = 0; l < NL; ++l) {
             const float* LW = W + l * LAYER_FLOATS;
-            const float* lg = LG + l * J * J;
             // ---- x = x + MHA(LN0(x))   (GraAttenLayer, GraFormer.py:94-95)
-            layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
+            if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
             __syncthreads();
-            {
-                const float* bias = LW + OFF_BQKV;
-                gemm_wg<18, 6, 0>(B1, LDX, nullptr, 0, LW + OFF_QKV, wave, lane,
-                                  [&](int r, int c, float v) { B2[r * LD2 + c] = v + bias[c]; });
+            if (DPK_RUN(16 | 32)) {
+                const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
+                gemm_wg<18, 6, 0, E_STORE>(B1, LDX, nullptr, 0, LW + OFF_QKV, wave, lane, e);
             }
             __syncthreads();
-            attention(B2, B1, a.mask, tid);
+            if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
             __syncthreads();
-            {
-                const float* bias = LW + OFF_BO;
-                gemm_wg<6, 6, 0>(B1, LDX, nullptr, 0, LW + OFF_O, wave, lane,
-                                 [&](int r, int c, float v) { XS[r * LDX + c] = XS[r * LDX + c] + (v + bias[c]); });
+            if (DPK_RUN(16 | 64)) {
+                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
+                gemm_wg<6, 6, 0, E_RESID>(B1, LDX, nullptr, 0, LW + OFF_O, wave, lane, e);
             }
             __syncthreads();
-            // ---- x = x + GraphNet(LN1(x))   (GraFormer.py:189-201)
-            layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
+            // ---- x = x + GraphNet(LN1(x)) = x + L (relu((L LN1(x)) W1^T + b1) W2^T) + b2
+            //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
+            if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
             __syncthreads();
-            graph_apply<2>(lg, B1, LDX, B1, LDX, D, tid);
+            if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
             __syncthreads();
-            {
-                const float* bias = LW + OFF_BFC1;
-                gemm_wg<12, 6, 0>(B1, LDX, nullptr, 0, LW + OFF_FC1, wave, lane,
-                                  [&](int r, int c, float v) { B2[r * LD2 + c] = fmaxf(v + bias[c], 0.f); });
+            if (DPK_RUN(16 | 128)) {
+                const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
+                gemm_wg<12, 6, 0, E_STORE_RELU>(B1, LDX, nullptr, 0, LW + OFF_FC1, wave, lane, e);
             }
             __syncthreads();
-            graph_apply<4>(lg, B2, LD2, B2, LD2, D2, tid);
-            __syncthreads();
-            {
-                const float* bias = LW + OFF_BFC2;
-                gemm_wg<6, 12, 0>(B2, LD2, nullptr, 0, LW + OFF_FC2, wave, lane,
-                                  [&](int r, int c, float v) { XS[r * LDX + c] = XS[r * LDX + c] + (v + bias[c]); });
+            if (DPK_RUN(16 | 256)) {
+                const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
+                gemm_wg<6, 12, 0, E_STORE_NB>(B2, LD2, nullptr, 0, LW + OFF_FC2, wave, lane, e);
             }
+            __syncthreads();
+            if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
             __syncthreads();
             // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
-            cheb_prep(T1, T2, XS, B2, tid);
+            if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
             __syncthreads();
-            {
-                const float* bias = LW + OFF_BC1;
+            if (DPK_RUN(16 | 512)) {
                 const float* tp = a.tproj + (EPS_MODE ? 0 : (size_t)s * NL * D) + l * D;
-                const int pstride = EPS_MODE ? NL * D : 0;
-                gemm_wg<6, 6, 12>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, [&](int r, int c, float v) {
-                    const float* tpp = tp + (size_t)(EPS_MODE ? min(pose0 + r / J, a.N - 1) : 0) * pstride;
-                    B1[r * LDX + c] = fmaxf(v + bias[c], 0.f) + tpp[c];
-                });
+                const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
+                gemm_wg<6, 6, 12, E_CHEB1>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, e);
             }
             __syncthreads();
-            cheb_prep(T1, T2, B1, B2, tid);
+            if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
             __syncthreads();
-            {
-                const float* bias = LW + OFF_BC2;
-                gemm_wg<6, 6, 12>(B1, LDX, B2, LD2, LW + OFF_C2, wave, lane, [&](int r, int c, float v) {
-                    XS[r * LDX + c] = XS[r * LDX + c] + fmaxf(v + bias[c], 0.f);
-                });
+            if (DPK_RUN(16 | 1024)) {
+                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
+                gemm_wg<6, 6, 12, E_RESID_RELU>(B1, LDX, B2, LD2, LW + OFF_C2, wave, lane, e);
             }
             __syncthreads();
         }
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
-        cheb_prep(T1, T2, XS, B2, tid);
+        cheb_prep<SPARSE>(CW, XS, B2, tid);
         __syncthreads();
         {
-            const float* bias = W + OFF_BOUT;
             const f32x4* Bo = reinterpret_cast<const f32x4*>(W + OFF_WOUT);
-            const float* cf = a.coef + (EPS_MODE ? 0 : s * 6);
+            const float* cfp = a.coef + (EPS_MODE ? 0 : s * 6);
+            const float cf[5] = {cfp[0], cfp[1], cfp[2], cfp[3], cfp[4]};   // uniform: SGPRs
+            const float bo = W[OFF_BOUT + (lane & 15)];
             auto epi = [&](int r, int c, float v) {
-                if (c >= COUT) return;
-                const float et = v + bias[c];
+                const float et = v + bo;
                 const int idx = r * CIN + c;           // same as r*COUT+c (coords 5 -> 5)
                 const bool valid = idx < nvalid;
                 const size_t gidx = (size_t)pose0 * PE + idx;
@@ -575,8 +811,8 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
                     }
                 }
             };
-            gemm_wave<1, 1, 6, 12>(XS, LDX, B2, LD2, Bo, wave, 0, lane, epi);
-            if (wave == 3) gemm_wave<1, 1, 6, 12>(XS, LDX, B2, LD2, Bo, 4, 0, lane, epi);
+            gemm_out<1, 6, 12>(XS, LDX, B2, LD2, Bo, wave, lane, epi);
+            if (wave == 3) gemm_out<1, 6, 12>(XS, LDX, B2, LD2, Bo, 4, lane, epi);
         }
         __syncthreads();
     }
@@ -664,6 +900,7 @@ struct dpk_handle {
     unsigned mask = (1u << J) - 1u;
     std::vector<float> h_adj;
     bool profiling = false;
+    bool sparse_graph = false;     // adjacency matches the compiled H36M Chebyshev pattern
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
 };
 
@@ -800,9 +1037,24 @@ int dpk_set_graph(dpk_handle* h, const float* adj) {
     float T1[J * J], T2[J * J];
     cheb_terms(adj, T1, T2);
     for (int i = 0; i < J * J; ++i) {
-        h->h_arena[OFF_T1 + i] = T1[i];
-        h->h_arena[OFF_T2 + i] = T2[i];
+        h->h_arena[OFF_CHEB + i] = T1[i];
+        h->h_arena[OFF_CHEB + J * J + i] = T2[i];
     }
+    // sparse path iff every nonzero of T1/T2 lies inside the compiled H36M pattern
+    bool fits = true;
+    for (int i = 0; i < J; ++i)
+        for (int j = 0; j < J; ++j) {
+            bool in1 = false, in2 = false;
+            for (int k = 0; k < SPAT.n1[i]; ++k) in1 = in1 || SPAT.c1[i][k] == j;
+            for (int k = 0; k < SPAT.n2[i]; ++k) in2 = in2 || SPAT.c2[i][k] == j;
+            if ((!in1 && T1[i * J + j] != 0.f) || (!in2 && T2[i * J + j] != 0.f)) fits = false;
+        }
+    for (int i = 0; i < J; ++i) {
+        for (int k = 0; k < SPAT.n1[i]; ++k) h->h_arena[OFF_CHEBS + SPAT.o1[i] + k] = T1[i * J + SPAT.c1[i][k]];
+        for (int k = 0; k < SPAT.n2[i]; ++k)
+            h->h_arena[OFF_CHEBS + SPAT.nnz1 + SPAT.o2[i] + k] = T2[i * J + SPAT.c2[i][k]];
+    }
+    h->sparse_graph = fits;
     h->h_adj.assign(adj, adj + J * J);
     h->have_graph = true;
     if (h->have_weights) return upload(h);
@@ -1012,7 +1264,10 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     a.mask = h->mask;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
-    hipLaunchKernelGGL(sample_kernel<true>, dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    if (h->sparse_graph)
+        hipLaunchKernelGGL((sample_kernel<true, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((sample_kernel<true, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -1048,7 +1303,10 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.seed = seed;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    hipLaunchKernelGGL(sample_kernel<false>, dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    if (h->sparse_graph)
+        hipLaunchKernelGGL((sample_kernel<false, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((sample_kernel<false, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return DPK_OK;

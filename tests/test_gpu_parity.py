@@ -178,3 +178,29 @@ def test_bad_inputs_raise(model, mask):
         model(torch.zeros(2, 16, 5, device="cuda:0"), mask, torch.zeros(2, device="cuda:0"), 0)
     with pytest.raises(Exception):
         model.sample(torch.zeros(2, 17, 5, device="cuda:0"), [0, 60], _betas(51))  # t+1 beyond table
+
+
+def test_non_h36m_graph_dense_path(mask):
+    """An adjacency outside the compiled H36M Chebyshev pattern runs the dense graph path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from oracle import gcndiff_oracle as O
+    from diffpose_amd.gcndiff import H36M_EDGES
+
+    edges = tuple(H36M_EDGES) + ((3, 16), (6, 13))
+    adj = adj_mx_from_edges(17, edges)
+    sd = synthetic_state_dict()
+    m = HipGCNdiff(adj, None, device="cuda:0")
+    m.load_state_dict(sd)
+    x, _ = synthetic_batch(9, seed=77)
+    t = torch.tensor([49., 3., 17., 0., 8., 49., 22., 31., 5.])
+    eps = m(torch.from_numpy(x).cuda(), mask, t.cuda(), 0)
+    ref = O.gcndiff_forward(O.params_to_torch(sd), O.adjacency(17, edges), torch.from_numpy(x),
+                            torch.ones(1, 1, 17, dtype=torch.bool), t)
+    assert _maxdiff(eps, ref) <= EPS_TOL
+    seq = make_seq("uniform", 50, 10)
+    out = m.sample(torch.from_numpy(x).cuda(), seq, _betas(51), mask=mask)
+    xs, _ = O.generalized_steps(torch.from_numpy(x), torch.ones(1, 1, 17, dtype=torch.bool), seq,
+                                lambda a_, m_, t_: O.gcndiff_forward(O.params_to_torch(sd), O.adjacency(17, edges),
+                                                                     a_, m_, t_), _betas(51))
+    assert _maxdiff(out, xs[-1]) <= TRAJ_TOL
