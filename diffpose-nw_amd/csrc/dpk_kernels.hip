@@ -6,10 +6,10 @@
 // only HBM traffic is the (N,17,5) input, the output and the weights (L2/MALL-resident).
 //
 // Tile geometry: 4 poses = 68 rows of 96 features; Linear/ChebConv
-// GEMMs run on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 fma chains) over 5 row
-// tiles of 16; waves 0-2 own column thirds of row tiles 0-3, wave 3 owns row tile 4
-// (rows 64-67 valid).  LayerNorm, 17-joint attention and the 17x17 graph products are
-// VALU work between workgroup barriers.  Weights are repacked at load time into MFMA
+// GEMMs run on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 fma chains) over 4 row tiles
+// of 16 (each wave: 2 row tiles x half the columns), the 4 leftover rows on the VALU inside
+// the same k-loop.  LayerNorm, 17-joint attention and the 17x17 graph products are VALU
+// work between workgroup barriers.  Weights are repacked at load time into MFMA
 // B-fragment order: one 1 KiB coalesced float4-per-lane load per (16 cols x 16 k) block.
 #include <hip/hip_runtime.h>
 
@@ -53,8 +53,8 @@ constexpr int PE = J * CIN;  // floats per pose (85)
 // workgroup tile
 constexpr int P = 4;         // poses per workgroup
 constexpr int R = P * J;     // 68 rows
-constexpr int RT = 5;        // 16-row MFMA tiles covering R (80 rows, 64..67 valid in the last)
 constexpr int NT = 256;      // threads (4 waves, one per SIMD)
+constexpr int NW = NT / 64;
 constexpr int LDX = 104;     // LDS row stride, 96-wide buffers  (≡40 mod 64: conflict-free b128 A reads)
 constexpr int LD2 = 296;     // LDS row stride, 288-wide buffer  (≡40 mod 64)
 
@@ -109,6 +109,11 @@ constexpr float SQRT_DK = 4.898979485566356f;   // float(math.sqrt(24)), divisor
 constexpr float LN_EPS = 1e-6f;                         // LayerNorm eps (GraFormer.py:60)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// packed fp32 fma (v_pk_fma_f32: two lanes of work per instruction)
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
 
 struct SampleArgs {
     const float* arena;   // packed weights
@@ -167,46 +172,92 @@ __device__ __forceinline__ int opaque(int x) {
 }
 
 // ---------------------------------------------------------------------------------------
-// MFMA GEMM over one wave's units: row tiles [rt0, rt0+NR) x col tiles [ct0, ct0+NCW).
-// A: LDS rows (k in [0,16*KB0) from A0, [16*KB0, 16*(KB0+KB1)) from A1); B: packed blocks.
-// Lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for MFMA sub-step j, and the
-// packed B block holds W[k = same][n = ct*16 + (l&15)]: a consistent permutation of k.
-// rt0/ct0 are wave-uniform (SGPR): B addresses are scalar base + lane*16.  The k-loop is a
-// 2-stage register ring (named buffers, unrolled by 2): the B (global/L2) and A (LDS)
-// fragments of k-block kb+1 are in flight while the MFMAs of kb issue.
-template <int NR, int NCW, int KB0, int KB1>
+// GEMM over the workgroup's 68 rows.  Rows 0..63 are 4 MFMA row tiles (v_mfma_f32_16x16x4_f32);
+// the 4 leftover rows 64..67 ("tail") are computed on the VALU inside the same k-loop from the
+// B fragments already in registers, so no MFMA work is spent on padding rows.
+//
+// MFMA operand maps: lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for sub-step j,
+// and the packed B block holds W[k = same][n = ct*16 + (l&15)] (a consistent permutation of k).
+// Tail: lane l accumulates, for tail row t and its column (l&15) of col tile c, the partial sum
+// over its own 4 k's of every k-block; the 4 lane groups are summed with two xor-shuffles.
+//
+// Wave w owns row tiles {2*(w>>1), 2*(w>>1)+1}, col tiles [(w&1)*NC/2, (w&1+1)*NC/2) and tail
+// rows 64 + 2*(w>>1) + {0,1} over the same columns: the four waves carry equal work.
+// The k-loop is a 2-stage register ring (named buffers, unrolled by 2): the B (global/L2) and
+// A (LDS) fragments of k-block kb+1 are in flight while the MFMAs of kb issue.
+template <int NR, int NCW, int TR, int KB0, int KB1>
 struct GemmTile {
     static constexpr int KB = KB0 + KB1;
+    static constexpr int TA = TR > 0 ? TR : 1;
     f32x4 acc[NR][NCW];
-    int aoff0[NR], aoff1[NR];
+    f32x2 tl[NCW][TA];      // tail partial sums: (.x, .y) = even / odd k of this lane's k's
+    int aoff0[NR], aoff1[NR], toff0[TA], toff1[TA];
 
-    __device__ __forceinline__ void load(f32x4 (&a)[NR], f32x4 (&b)[NCW], const float* A0, const float* A1,
-                                         const f32x4* __restrict__ Bl, int kb) const {
-#pragma unroll
-        for (int c = 0; c < NCW; ++c) b[c] = Bl[(c * KB + kb) * 64];
+    __device__ __forceinline__ void loadA(f32x4 (&a)[NR], f32x4 (&t)[TA], const float* A0, const float* A1,
+                                          int kb) const {
         if (kb < KB0) {
 #pragma unroll
             for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A0 + aoff0[i] + kb * 16);
+#pragma unroll
+            for (int i = 0; i < TR; ++i) t[i] = *reinterpret_cast<const f32x4*>(A0 + toff0[i] + kb * 16);
         } else {
 #pragma unroll
-            for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A1 + aoff1[i] + (kb - KB0) * 16);
+            for (int i = 0; i < NR; ++i)
+                a[i] = *reinterpret_cast<const f32x4*>(A1 + aoff1[i] + (kb - KB0) * 16);
+#pragma unroll
+            for (int i = 0; i < TR; ++i)
+                t[i] = *reinterpret_cast<const f32x4*>(A1 + toff1[i] + (kb - KB0) * 16);
         }
     }
-    __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&b)[NCW]) {
+    __device__ __forceinline__ static void loadB(f32x4 (&b)[NCW], const f32x4* __restrict__ Bl, int kb) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int c = 0; c < NCW; ++c) b[c] = Bl[(c * KB + kb) * 64];
+    }
+    __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&t)[TA], const f32x4 (&b)[NCW]) {
 #pragma unroll
-            for (int i = 0; i < NR; ++i)
+        for (int jp = 0; jp < 4; jp += 2) {
 #pragma unroll
-                for (int c = 0; c < NCW; ++c)
-                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+            for (int j = jp; j < jp + 2; ++j)
+#pragma unroll
+                for (int i = 0; i < NR; ++i)
+#pragma unroll
+                    for (int c = 0; c < NCW; ++c)
+                        acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < NCW; ++c)
+#pragma unroll
+                for (int r = 0; r < TR; ++r)
+                    tl[c][r] = pfma(f32x2{t[r][jp], t[r][jp + 1]}, f32x2{b[c][jp], b[c][jp + 1]}, tl[c][r]);
+        }
     }
 };
+
+// B fragments of a GEMM's first two k-blocks, loaded before the phase that precedes the GEMM
+// (weights do not depend on activations) so the L2 latency hides under that phase.
+template <int NCW>
+struct BPre {
+    f32x4 b0[NCW], b1[NCW];
+};
+
+// Column tiles per streamed pass (see gemm_stream).
+constexpr int CW = 3;
+
+template <int NC, int KB>
+__device__ __forceinline__ BPre<NC / 2> gemm_prefetch(const float* Bp, int wave, int lane) {
+    BPre<NC / 2> pre;
+    const f32x4* Bl = reinterpret_cast<const f32x4*>(Bp) + (size_t)((wave & 1) * (NC / 2)) * KB * 64 + lane;
+#pragma unroll
+    for (int c = 0; c < NC / 2; ++c) {
+        pre.b0[c] = Bl[(c * KB + 0) * 64];
+        pre.b1[c] = KB > 1 ? Bl[(c * KB + 1) * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    return pre;
+}
 
 // Epilogue modes (out = acc + bias[col]):
 //   E_STORE       dst = out                       (QKV, gconv_input)
 //   E_STORE_RELU  dst = relu(out)                 (GraphNet fc1)
-//   E_RESID       dst = dst + out                 (attention O-proj, GraphNet fc2)
+//   E_RESID       dst = dst + out                 (attention O-proj)
 //   E_RESID_RELU  dst = dst + relu(out)           (Cheb2 of _ResChebGC_diff)
 //   E_CHEB1       dst = relu(out) + tproj[col]    (Cheb1 + temb_proj injection)
 //   E_STORE_NB    dst = acc (no bias)             (GraphNet fc2 before its graph product)
@@ -224,58 +275,85 @@ struct EpiArgs {
     int pose_max;           // N-1
 };
 
-template <int NR, int NCW, int KB0, int KB1, int MODE, bool PARTIAL>
+template <int MODE>
+__device__ __forceinline__ float epi_value(float acc, float bias, float tp, float old) {
+    const float v = acc + bias;
+    if constexpr (MODE == E_STORE_NB) return acc;
+    else if constexpr (MODE == E_STORE) return v;
+    else if constexpr (MODE == E_STORE_RELU) return fmaxf(v, 0.f);
+    else if constexpr (MODE == E_RESID) return old + v;
+    else if constexpr (MODE == E_RESID_RELU) return old + fmaxf(v, 0.f);
+    else return fmaxf(v, 0.f) + tp;
+}
+
+__device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, float tcol) {
+    if (e.tproj_pose_stride == 0) return tcol;
+    const int pose = min(e.pose0 + row / J, e.pose_max);
+    return e.tproj[(size_t)pose * e.tproj_pose_stride + col];
+}
+
+// One wave, single pass: row tiles [rt0, rt0+NR) on MFMA and tail rows trow0.. on VALU over
+// NCW column tiles from ct0; 2-stage register ring (named buffers, unrolled by 2).  Used for
+// the wide GEMMs (QKV: 9, fc1: 6 column tiles per wave).
+template <int NR, int NCW, int TR, int KB0, int KB1, int MODE>
 __device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float* A1, int lda1,
-                                          const f32x4* __restrict__ Bp, int rt0, int ct0, int lane,
-                                          const EpiArgs& e) {
-    using T = GemmTile<NR, NCW, KB0, KB1>;
+                                          const f32x4* __restrict__ Bp, int rt0, int ct0, int trow0, int lane,
+                                          const EpiArgs& e, const BPre<NCW>& pre) {
+    using T = GemmTile<NR, NCW, TR, KB0, KB1>;
     constexpr int KB = T::KB;
+    constexpr int TA = T::TA;
+    static_assert(KB % 2 == 0, "k-blocks in pairs");
     lane = opaque(lane);
     T g;
 #pragma unroll
     for (int i = 0; i < NR; ++i)
 #pragma unroll
         for (int c = 0; c < NCW; ++c) g.acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCW; ++c)
+#pragma unroll
+        for (int r = 0; r < TA; ++r) g.tl[c][r] = f32x2{0.f, 0.f};
     const int rl = lane & 15, kq = (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-        int r = (rt0 + i) * 16 + rl;
-        r = r < R ? r : R - 1;          // clamp padding rows (outputs discarded)
+        const int r = (rt0 + i) * 16 + rl;
         g.aoff0[i] = r * lda0 + kq;
         g.aoff1[i] = r * lda1 + kq;
+    }
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+        g.toff0[i] = (trow0 + i) * lda0 + kq;
+        g.toff1[i] = (trow0 + i) * lda1 + kq;
     }
     float bcol[NCW], tcol[NCW];
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
-        bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[(ct0 + c) * 16 + rl];
-        tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[(ct0 + c) * 16 + rl] : 0.f;
+        const int col = (ct0 + c) * 16 + rl;
+        bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[col];
+        tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
     }
     const f32x4* Bl = Bp + (size_t)ct0 * KB * 64 + lane;
-    f32x4 a0[NR], b0[NCW];
-    g.load(a0, b0, A0, A1, Bl, 0);
-    if constexpr (KB == 1) {
-        g.mma(a0, b0);
-    } else {
-        static_assert(KB % 2 == 0, "k-blocks in pairs");
-        f32x4 a1[NR], b1[NCW];
+    f32x4 a0[NR], t0[TA], b0[NCW], a1[NR], t1[TA], b1[NCW];
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+        b0[c] = pre.b0[c];
+        b1[c] = pre.b1[c];
+    }
+    g.loadA(a0, t0, A0, A1, 0);
+    g.loadA(a1, t1, A0, A1, 1);
 #pragma unroll 1
-        for (int kb = 0; kb < KB; kb += 2) {
-            g.load(a1, b1, A0, A1, Bl, kb + 1);
-            g.mma(a0, b0);
-            if (kb + 2 < KB) g.load(a0, b0, A0, A1, Bl, kb + 2);
-            g.mma(a1, b1);
+    for (int kb = 0; kb < KB; kb += 2) {
+        g.mma(a0, t0, b0);
+        if (kb + 2 < KB) {
+            T::loadB(b0, Bl, kb + 2);
+            g.loadA(a0, t0, A0, A1, kb + 2);
+        }
+        g.mma(a1, t1, b1);
+        if (kb + 3 < KB) {
+            T::loadB(b1, Bl, kb + 3);
+            g.loadA(a1, t1, A0, A1, kb + 3);
         }
     }
-    if (DPK_EXP & 1) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < NCW; ++c) asm volatile("" ::"v"(g.acc[i][c]));
-        return;
-    }
-    // C/D map of 16x16 MFMA: col = lane&15, row = 4*(lane>>4) + r.  The partial tile (rows
-    // 64..79 of which 64..67 exist) keeps lanes 0-15 only.
-    if (PARTIAL && kq != 0) return;
     float* d = e.dst + ((rt0 * 16 + kq) * e.ldd + ct0 * 16 + rl);
     float old[NR][NCW][4];
     if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
@@ -292,78 +370,254 @@ __device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float
         for (int c = 0; c < NCW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float v = g.acc[i][c][r] + bcol[c];
-                float o;
-                if constexpr (MODE == E_STORE_NB) o = g.acc[i][c][r];
-                else if constexpr (MODE == E_STORE) o = v;
-                else if constexpr (MODE == E_STORE_RELU) o = fmaxf(v, 0.f);
-                else if constexpr (MODE == E_RESID) o = old[i][c][r] + v;
-                else if constexpr (MODE == E_RESID_RELU) o = old[i][c][r] + fmaxf(v, 0.f);
-                else {
-                    float tp = tcol[c];
-                    if (e.tproj_pose_stride != 0) {
-                        const int pose = min(e.pose0 + ((rt0 + i) * 16 + kq + r) / J, e.pose_max);
-                        tp = e.tproj[(size_t)pose * e.tproj_pose_stride + (ct0 + c) * 16 + rl];
-                    }
-                    o = fmaxf(v, 0.f) + tp;
-                }
-                d[(i * 16 + r) * e.ldd + c * 16] = o;
+                const int row = (rt0 + i) * 16 + kq + r;
+                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (ct0 + c) * 16 + rl, tcol[c]) : 0.f;
+                d[(i * 16 + r) * e.ldd + c * 16] = epi_value<MODE>(
+                    g.acc[i][c][r], bcol[c], tp, (MODE == E_RESID || MODE == E_RESID_RELU) ? old[i][c][r] : 0.f);
             }
-}
-
-// Whole-workgroup GEMM with NC (multiple of 3) output col tiles.  `wave` must be uniform.
-template <int NC, int KB0, int KB1, int MODE>
-__device__ __forceinline__ void gemm_wg(const float* A0, int lda0, const float* A1, int lda1, const float* Bp,
-                                        int wave, int lane, const EpiArgs& e) {
-    static_assert(NC % 3 == 0, "column tiles split in thirds");
-    const f32x4* B = reinterpret_cast<const f32x4*>(Bp);
-    if (wave < 3) {
-        gemm_wave<4, NC / 3, KB0, KB1, MODE, false>(A0, lda0, A1, lda1, B, 0, wave * (NC / 3), lane, e);
-    } else if (!(DPK_EXP & 2)) {
-        // wave 3: the partial row tile across all columns, in passes of <= 12 column tiles
-        constexpr int CH = NC <= 12 ? NC : NC / 2;
-        static_assert(NC % CH == 0, "column chunking");
-#pragma unroll 1
-        for (int c0 = 0; c0 < NC; c0 += CH)
-            gemm_wave<1, CH, KB0, KB1, MODE, true>(A0, lda0, A1, lda1, B, 4, c0, lane, e);
+    if constexpr (TR > 0) {
+        float tv[NCW][TR];
+#pragma unroll
+        for (int c = 0; c < NCW; ++c)
+#pragma unroll
+            for (int r = 0; r < TR; ++r) {
+                float v = g.tl[c][r].x + g.tl[c][r].y;
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                tv[c][r] = v;
+            }
+        const int grp = lane >> 4;
+        if (grp < TR) {
+            const int row = trow0 + grp;
+            float* dt = e.dst + row * e.ldd + ct0 * 16 + rl;
+#pragma unroll
+            for (int c = 0; c < NCW; ++c) {
+                float v = tv[c][0];
+#pragma unroll
+                for (int r = 1; r < TR; ++r)
+                    if (grp == r) v = tv[c][r];
+                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[c * 16] : 0.f;
+                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (ct0 + c) * 16 + rl, tcol[c]) : 0.f;
+                dt[c * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
+            }
+        }
     }
 }
 
-// Output ChebConv (96->5, one col tile): raw accumulators handed to a functor (DDIM update).
-template <int NR, int KB0, int KB1, class Epi>
-__device__ __forceinline__ void gemm_out(const float* A0, int lda0, const float* A1, int lda1,
-                                         const f32x4* __restrict__ Bp, int rt0, int lane, Epi epi) {
-    using T = GemmTile<NR, 1, KB0, KB1>;
+// One wave, streamed: row tile rt on MFMA and tail row trow on VALU, over NP passes of CW column
+// tiles starting at ct0.  B/A/tail operands flow through a 3-stage register ring (named
+// buffers, loop unrolled by 3): step i computes with slot i%3 while slots (i+1)%3 and (i+2)%3
+// are in flight; passes are chained so the next pass's first fragments load under the
+// current pass's last MFMAs and epilogue.
+template <int NR, int TR, int NP, int KB0, int KB1, int MODE>
+__device__ __forceinline__ void gemm_stream(const float* A0, int lda0, const float* A1, int lda1,
+                                            const f32x4* __restrict__ Bp, int rt, int ct0, int trow, int lane,
+                                            const EpiArgs& e, const BPre<CW>& pre) {
+    using T = GemmTile<NR, CW, TR, KB0, KB1>;
     constexpr int KB = T::KB;
+    constexpr int NS = NP * KB;                  // steps
+    static_assert(KB == 1 || KB % 3 == 0, "pass boundary at ring position 2");
     lane = opaque(lane);
     T g;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) g.acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int rl = lane & 15, kq = (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-        int r = (rt0 + i) * 16 + rl;
-        r = r < R ? r : R - 1;
+        const int r = (rt + i) * 16 + rl;
         g.aoff0[i] = r * lda0 + kq;
         g.aoff1[i] = r * lda1 + kq;
     }
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+        g.toff0[i] = (trow + i) * lda0 + kq;
+        g.toff1[i] = (trow + i) * lda1 + kq;
+    }
+    auto zero = [&]() {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) g.acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < TR; ++i) g.tl[c][i] = f32x2{0.f, 0.f};
+        }
+    };
+    zero();
+    const f32x4* Bl = Bp + (size_t)ct0 * KB * 64 + lane;
+    // B block of step i: pass i/KB, kb i%KB -> column tiles ct0 + CW*pass + c
+    auto loadB = [&](f32x4 (&b)[CW], int i) {
+        const int pass = i / KB, kb = i - pass * KB;
+#pragma unroll
+        for (int c = 0; c < CW; ++c) b[c] = Bl[((pass * CW + c) * KB + kb) * 64];
+    };
+    auto loadA = [&](f32x4 (&a)[NR], f32x4 (&t)[TR], int i) { g.loadA(a, t, A0, A1, i % KB); };
+
+    // epilogue of pass `pass` (rows: MFMA tile + tail row)
+    auto epilogue = [&](int pass) {
+        const int cb = ct0 + pass * CW;
+        float bcol[CW], tcol[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const int col = (cb + c) * 16 + rl;
+            bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[col];
+            tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
+        }
+        float* d = e.dst + ((rt * 16 + kq) * e.ldd + cb * 16 + rl);
+        float old[NR][CW][4];
+        if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i)
+#pragma unroll
+                for (int c = 0; c < CW; ++c)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + c * 16];
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < CW; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = (rt + i) * 16 + kq + r;
+                    const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (cb + c) * 16 + rl, tcol[c]) : 0.f;
+                    d[(i * 16 + r) * e.ldd + c * 16] = epi_value<MODE>(
+                        g.acc[i][c][r], bcol[c], tp, (MODE == E_RESID || MODE == E_RESID_RELU) ? old[i][c][r] : 0.f);
+                }
+        // tail rows: reduce the 4 lane groups' k-partials; lane group t writes tail row t
+        float tv[CW][TR];
+#pragma unroll
+        for (int c = 0; c < CW; ++c)
+#pragma unroll
+            for (int i = 0; i < TR; ++i) {
+                float v = g.tl[c][i].x + g.tl[c][i].y;
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                tv[c][i] = v;
+            }
+        const int grp = lane >> 4;
+        if (grp < TR) {
+            const int row = trow + grp;
+            float* dt = e.dst + row * e.ldd + cb * 16 + rl;
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                float v = tv[c][0];
+#pragma unroll
+                for (int i = 1; i < TR; ++i)
+                    if (grp == i) v = tv[c][i];
+                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[c * 16] : 0.f;
+                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (cb + c) * 16 + rl, tcol[c]) : 0.f;
+                dt[c * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
+            }
+        }
+        zero();
+    };
+
+    f32x4 aS0[NR], tS0[TR], bS0[CW], aS1[NR], tS1[TR], bS1[CW], aS2[NR], tS2[TR], bS2[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        bS0[c] = pre.b0[c];
+        bS1[c] = pre.b1[c];
+    }
+    loadA(aS0, tS0, 0);
+    if constexpr (KB == 1) {                    // gconv_input: one k-block per pass
+        static_assert(NP == 1, "single pass");
+        g.mma(aS0, tS0, bS0);
+        epilogue(0);
+        return;
+    }
+    loadA(aS1, tS1, 1);
+#pragma unroll 1
+    for (int i = 0; i < NS; i += 3) {
+        if (i + 2 < NS) {
+            loadB(bS2, i + 2);
+            loadA(aS2, tS2, i + 2);
+        }
+        g.mma(aS0, tS0, bS0);
+        if (i + 3 < NS) {
+            loadB(bS0, i + 3);
+            loadA(aS0, tS0, i + 3);
+        }
+        g.mma(aS1, tS1, bS1);
+        if (i + 4 < NS) {
+            loadB(bS1, i + 4);
+            loadA(aS1, tS1, i + 4);
+        }
+        g.mma(aS2, tS2, bS2);
+        if ((i + 2) % KB == KB - 1) epilogue((i + 2) / KB);
+    }
+}
+
+// Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
+// 2*(w>>1)+1, column half w&1, tail rows 64 + 2*(w>>1) + {0,1}: equal work per wave, 128 B of
+// B fragment per MFMA; 2-stage single-pass register ring (the 3-stage streamed variant measured
+// slower for every shape here and is kept for the single-k-block gconv_input only).
+template <int NC, int KB0, int KB1, int MODE>
+__device__ __forceinline__ void gemm_wg(const float* A0, int lda0, const float* A1, int lda1, const float* Bp,
+                                        int wave, int lane, const EpiArgs& e, const BPre<NC / 2>& pre) {
+    static_assert(NC % 2 == 0 && R == 68 && NW == 4, "4 row tiles x 2 column halves + 4 tail rows");
+    const f32x4* B = reinterpret_cast<const f32x4*>(Bp);
+    const int half = wave >> 1;
+    if constexpr (KB0 + KB1 == 1)            // gconv_input: a single k-block
+        gemm_stream<2, 2, 1, KB0, KB1, MODE>(A0, lda0, A1, lda1, B, 2 * half, (wave & 1) * (NC / 2), 64 + 2 * half,
+                                             lane, e, pre);
+    else
+        gemm_wave<2, NC / 2, 2, KB0, KB1, MODE>(A0, lda0, A1, lda1, B, 2 * half, (wave & 1) * (NC / 2),
+                                                64 + 2 * half, lane, e, pre);
+}
+
+// Output ChebConv (96->5, one col tile): waves 0-3, wave w = row tile w + tail row 64+w; the
+// raw accumulators go to a functor (DDIM update).
+template <int KB>
+__device__ __forceinline__ BPre<1> out_prefetch(const float* Bp, int lane) {
+    BPre<1> pre;
+    const f32x4* Bl = reinterpret_cast<const f32x4*>(Bp) + lane;
+    pre.b0[0] = Bl[0];
+    pre.b1[0] = Bl[64];
+    return pre;
+}
+
+template <int KB0, int KB1, class Epi>
+__device__ __forceinline__ void gemm_out(const float* A0, int lda0, const float* A1, int lda1,
+                                         const f32x4* __restrict__ Bp, int wave, int lane, Epi epi,
+                                         const BPre<1>& pre) {
+    using T = GemmTile<1, 1, 1, KB0, KB1>;
+    constexpr int KB = T::KB;
+    lane = opaque(lane);
+    T g;
+    g.acc[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    g.tl[0][0] = f32x2{0.f, 0.f};
+    const int rl = lane & 15, kq = (lane >> 4) * 4;
+    {
+        const int r = wave * 16 + rl;
+        g.aoff0[0] = r * lda0 + kq;
+        g.aoff1[0] = r * lda1 + kq;
+        const int tr = 64 + wave;
+        g.toff0[0] = tr * lda0 + kq;
+        g.toff1[0] = tr * lda1 + kq;
+    }
     const f32x4* Bl = Bp + lane;
-    f32x4 a0[NR], b0[1], a1[NR], b1[1];
-    g.load(a0, b0, A0, A1, Bl, 0);
+    f32x4 a0[1], t0[1], b0[1] = {pre.b0[0]}, a1[1], t1[1], b1[1] = {pre.b1[0]};
+    g.loadA(a0, t0, A0, A1, 0);
+    g.loadA(a1, t1, A0, A1, 1);
 #pragma unroll 1
     for (int kb = 0; kb < KB; kb += 2) {
-        g.load(a1, b1, A0, A1, Bl, kb + 1);
-        g.mma(a0, b0);
-        if (kb + 2 < KB) g.load(a0, b0, A0, A1, Bl, kb + 2);
-        g.mma(a1, b1);
-    }
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int orow = (rt0 + i) * 16 + kq + r;
-            if (orow < R && rl < COUT) epi(orow, rl, g.acc[i][0][r]);
+        g.mma(a0, t0, b0);
+        if (kb + 2 < KB) {
+            T::loadB(b0, Bl, kb + 2);
+            g.loadA(a0, t0, A0, A1, kb + 2);
         }
+        g.mma(a1, t1, b1);
+        if (kb + 3 < KB) {
+            T::loadB(b1, Bl, kb + 3);
+            g.loadA(a1, t1, A0, A1, kb + 3);
+        }
+    }
+    float tv = g.tl[0][0].x + g.tl[0][0].y;
+    tv += __shfl_xor(tv, 16, 64);
+    tv += __shfl_xor(tv, 32, 64);
+    if (rl < COUT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) epi(wave * 16 + kq + r, rl, g.acc[0][0][r]);
+        if (kq == 0) epi(64 + wave, rl, tv);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -376,7 +630,10 @@ __device__ __forceinline__ float div_by(float x, float d, float r) {
 }
 
 // LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b, one pass:
-// 3 lanes per row (32 features each), 21 rows per wave; mean/var accumulated in double.
+// 3 lanes per row, 21 rows per wave.  Lane `part` of a row owns the 16-byte chunks
+// part, part+3, ..., part+21 (interleaved, so the three lanes of a row hit different LDS
+// banks).  Two-pass fp32 statistics, pairwise sums combined in the same order in all three
+// lanes (bitwise identical mean/std per row).
 __device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* __restrict__ gain,
                                            const float* __restrict__ shift, int tid) {
     tid = opaque(tid);
@@ -384,48 +641,48 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
     const int row = w * 21 + lane / 3, part = lane % 3;
     const bool ok = lane < 63 && row < R;
     const int rr = ok ? row : R - 1;
-    const float* s = src + rr * LDX + 32 * part;
-    float v[32];
+    const float* s = src + rr * LDX;
+    f32x4 v[8];
 #pragma unroll
-    for (int e = 0; e < 32; e += 4) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(s + e);
-        v[e] = t[0]; v[e + 1] = t[1]; v[e + 2] = t[2]; v[e + 3] = t[3];
-    }
+    for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const f32x4*>(s + 4 * (part + 3 * e));
+    auto psum = [](const f32x4 (&x)[8]) {
+        f32x4 a = (x[0] + x[1]) + (x[2] + x[3]);
+        f32x4 b = (x[4] + x[5]) + (x[6] + x[7]);
+        const f32x4 c = a + b;
+        return (c[0] + c[1]) + (c[2] + c[3]);
+    };
     const int base = (lane / 3) * 3;
-    double sum = 0.0;
+    const float ls = psum(v);
+    const float s0 = __shfl(ls, base, 64), s1 = __shfl(ls, base + 1, 64), s2 = __shfl(ls, base + 2, 64);
+    const float mean = ((s0 + s1) + s2) / (float)D;
+    f32x4 dv[8], sq[8];
 #pragma unroll
-    for (int e = 0; e < 32; ++e) sum += (double)v[e];
-    // identical combination order in the three lanes of a row
-    const double s0 = __shfl(sum, base, 64), s1 = __shfl(sum, base + 1, 64), s2 = __shfl(sum, base + 2, 64);
-    const double mean_d = ((s0 + s1) + s2) / (double)D;
-    double ss = 0.0;
-#pragma unroll
-    for (int e = 0; e < 32; ++e) {
-        const double dv = (double)v[e] - mean_d;
-        ss += dv * dv;
+    for (int e = 0; e < 8; ++e) {
+        dv[e] = v[e] - mean;
+        sq[e] = dv[e] * dv[e];
     }
-    const double q0 = __shfl(ss, base, 64), q1 = __shfl(ss, base + 1, 64), q2 = __shfl(ss, base + 2, 64);
-    const float mean = (float)mean_d;
-    const float den = (float)sqrt(((q0 + q1) + q2) / (double)(D - 1)) + LN_EPS;
+    const float lq = psum(sq);
+    const float q0 = __shfl(lq, base, 64), q1 = __shfl(lq, base + 1, 64), q2 = __shfl(lq, base + 2, 64);
+    const float den = sqrtf(((q0 + q1) + q2) / (float)(D - 1)) + LN_EPS;
     const float rcp = 1.0f / den;
     if (!ok) return;
-    float* d = dst + row * LDX + 32 * part;
+    float* d = dst + row * LDX;
 #pragma unroll
-    for (int e = 0; e < 32; e += 4) {
+    for (int e = 0; e < 8; ++e) {
+        const int c0 = 4 * (part + 3 * e);
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c0);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c0);
         f32x4 t;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = 32 * part + e + k;
-            t[k] = div_by(gain[c] * (v[e + k] - mean), den, rcp) + shift[c];
-        }
-        *reinterpret_cast<f32x4*>(d + e) = t;
+        for (int k = 0; k < 4; ++k) t[k] = div_by(gv[k] * dv[e][k], den, rcp) + sv[k];
+        *reinterpret_cast<f32x4*>(d + c0) = t;
     }
 }
 
 // 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
-// projections).  16 lanes per (pose, head): lane q owns query q (scores, softmax and PV in
-// registers); query 16 is computed cooperatively by the 16 lanes (one key each, group
-// reductions by shuffles).
+// projections).  16 lanes per (pose, head): lane q owns query q (scores, softmax and P.V in
+// registers, packed fp32 FMAs); query 16 is computed cooperatively by the 16 lanes (one key
+// each, group reductions by shuffles).
 __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
     tid = opaque(tid);
     const int grp = tid >> 4, q = tid & 15;
@@ -435,26 +692,26 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
     auto keyok = [&](int j) { return ((mask >> j) & 1u) != 0u; };
     // ---- query q
     {
-        float qv[DK];
+        f32x2 qv[DK / 2];
 #pragma unroll
         for (int d = 0; d < DK; d += 4) {
             const f32x4 t = *reinterpret_cast<const f32x4*>(rows + q * LD2 + d);
-            qv[d] = t[0]; qv[d + 1] = t[1]; qv[d + 2] = t[2]; qv[d + 3] = t[3];
+            qv[d / 2] = f32x2{t[0], t[1]};
+            qv[d / 2 + 1] = f32x2{t[2], t[3]};
         }
         float sc[J];
         float m = -INFINITY;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const float* kr = rows + j * LD2 + D;
-            float dot = 0.f;
+            f32x2 dot2 = {0.f, 0.f};
 #pragma unroll
             for (int d = 0; d < DK; d += 4) {
                 const f32x4 t = *reinterpret_cast<const f32x4*>(kr + d);
-                dot = fmaf(qv[d], t[0], dot);
-                dot = fmaf(qv[d + 1], t[1], dot);
-                dot = fmaf(qv[d + 2], t[2], dot);
-                dot = fmaf(qv[d + 3], t[3], dot);
+                dot2 = pfma(qv[d / 2], f32x2{t[0], t[1]}, dot2);
+                dot2 = pfma(qv[d / 2 + 1], f32x2{t[2], t[3]}, dot2);
             }
+            const float dot = dot2.x + dot2.y;
             sc[j] = keyok(j) ? dot / SQRT_DK : -1e9f;
             m = fmaxf(m, sc[j]);
         }
@@ -465,45 +722,43 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
             sum += sc[j];
         }
         const float inv = 1.0f / sum;
-        float o[DK];
+        f32x2 o[DK / 2];
 #pragma unroll
-        for (int d = 0; d < DK; ++d) o[d] = 0.f;
+        for (int d = 0; d < DK / 2; ++d) o[d] = f32x2{0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const float pj = sc[j] * inv;
+            const f32x2 pj = splat2(sc[j] * inv);
             const float* vr = rows + j * LD2 + 2 * D;
 #pragma unroll
             for (int d = 0; d < DK; d += 4) {
                 const f32x4 t = *reinterpret_cast<const f32x4*>(vr + d);
-                o[d] = fmaf(pj, t[0], o[d]);
-                o[d + 1] = fmaf(pj, t[1], o[d + 1]);
-                o[d + 2] = fmaf(pj, t[2], o[d + 2]);
-                o[d + 3] = fmaf(pj, t[3], o[d + 3]);
+                o[d / 2] = pfma(pj, f32x2{t[0], t[1]}, o[d / 2]);
+                o[d / 2 + 1] = pfma(pj, f32x2{t[2], t[3]}, o[d / 2 + 1]);
             }
         }
 #pragma unroll
         for (int d = 0; d < DK; d += 4)
-            *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+            *reinterpret_cast<f32x4*>(orows + q * LDX + d) =
+                f32x4{o[d / 2].x, o[d / 2].y, o[d / 2 + 1].x, o[d / 2 + 1].y};
     }
-    // ---- query 16: lane q scores key q (lane 0 also key 16)
+    // ---- query 16: lane q scores key q (lane 0's key-16 score broadcast)
     {
         const float* q16 = rows + 16 * LD2;
         auto score = [&](int j) {
             const float* kr = rows + j * LD2 + D;
-            float dot = 0.f;
+            f32x2 dot2 = {0.f, 0.f};
 #pragma unroll
             for (int d = 0; d < DK; d += 4) {
                 const f32x4 a4 = *reinterpret_cast<const f32x4*>(q16 + d);
                 const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + d);
-                dot = fmaf(a4[0], k4[0], dot);
-                dot = fmaf(a4[1], k4[1], dot);
-                dot = fmaf(a4[2], k4[2], dot);
-                dot = fmaf(a4[3], k4[3], dot);
+                dot2 = pfma(f32x2{a4[0], a4[1]}, f32x2{k4[0], k4[1]}, dot2);
+                dot2 = pfma(f32x2{a4[2], a4[3]}, f32x2{k4[2], k4[3]}, dot2);
             }
+            const float dot = dot2.x + dot2.y;
             return keyok(j) ? dot / SQRT_DK : -1e9f;
         };
         const float sq = score(q);
-        const float s16 = __shfl(score(16), 0, 16);        // every lane computes it; broadcast lane 0's
+        const float s16 = __shfl(score(16), 0, 16);
         float m = fmaxf(sq, s16);
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
@@ -514,7 +769,6 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
         sum += e16;
         const float inv = 1.0f / sum;
         const float pq = eq * inv, p16 = e16 * inv;
-        // output dims d = q and d = q + 16 (q < 8): o_d = sum_j P_j V[j][d]
         float o0 = 0.f, o1 = 0.f;
         const float* vcol = rows + 2 * D;
 #pragma unroll
@@ -585,41 +839,27 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
     if (tid >= P * ng) return;
     const int p = tid / ng;
     const int c = (tid - p * ng) * G;
-    float v[J][G];
+    f32x2 v[J];
 #pragma unroll
-    for (int i = 0; i < J; ++i) {
-        const float2 t = *reinterpret_cast<const float2*>(src + (p * J + i) * LDX + c);
-        v[i][0] = t.x;
-        v[i][1] = t.y;
-    }
+    for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
+        f32x2 t1 = {0.f, 0.f}, t2 = {0.f, 0.f};
         if constexpr (SPARSE) {
 #pragma unroll
-            for (int k = 0; k < SPAT.n1[j]; ++k) {
-                const float w = cw[SPAT.o1[j] + k];
-                a0 = fmaf(w, v[SPAT.c1[j][k]][0], a0);
-                a1 = fmaf(w, v[SPAT.c1[j][k]][1], a1);
-            }
+            for (int k = 0; k < SPAT.n1[j]; ++k) t1 = pfma(splat2(cw[SPAT.o1[j] + k]), v[SPAT.c1[j][k]], t1);
 #pragma unroll
-            for (int k = 0; k < SPAT.n2[j]; ++k) {
-                const float w = cw[SPAT.nnz1 + SPAT.o2[j] + k];
-                c0 = fmaf(w, v[SPAT.c2[j][k]][0], c0);
-                c1 = fmaf(w, v[SPAT.c2[j][k]][1], c1);
-            }
+            for (int k = 0; k < SPAT.n2[j]; ++k)
+                t2 = pfma(splat2(cw[SPAT.nnz1 + SPAT.o2[j] + k]), v[SPAT.c2[j][k]], t2);
         } else {
 #pragma unroll
             for (int i = 0; i < J; ++i) {
-                const float t1 = cw[j * J + i], t2 = cw[J * J + j * J + i];
-                a0 = fmaf(t1, v[i][0], a0);
-                a1 = fmaf(t1, v[i][1], a1);
-                c0 = fmaf(t2, v[i][0], c0);
-                c1 = fmaf(t2, v[i][1], c1);
+                t1 = pfma(splat2(cw[j * J + i]), v[i], t1);
+                t2 = pfma(splat2(cw[J * J + j * J + i]), v[i], t2);
             }
         }
-        *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + c) = make_float2(a0, a1);
-        *reinterpret_cast<float2*>(b2 + (p * J + j) * LD2 + D + c) = make_float2(c0, c1);
+        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
+        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
     }
 }
 
@@ -635,33 +875,21 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
     if (tid >= P * ng) return;
     const int p = tid / ng;
     const int c = (tid - p * ng) * G;
-    float v[J][G];
+    f32x2 v[J];
 #pragma unroll
-    for (int i = 0; i < J; ++i) {
-        const float2 t = *reinterpret_cast<const float2*>(src + (p * J + i) * LDX + c);
-        v[i][0] = t.x;
-        v[i][1] = t.y;
-    }
-    float b0 = 0.f, b1 = 0.f;
-    if (RESID) {
-        b0 = bias[c];
-        b1 = bias[c + 1];
-    }
+    for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
+    f32x2 bb = {0.f, 0.f};
+    if (RESID) bb = *reinterpret_cast<const f32x2*>(bias + c);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        float a0 = 0.f, a1 = 0.f;
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < J; ++i) {
-            const float w = L[j * J + i];
-            a0 = fmaf(w, v[i][0], a0);
-            a1 = fmaf(w, v[i][1], a1);
-        }
-        float2* o = reinterpret_cast<float2*>(dst + (p * J + j) * LDX + c);
+        for (int i = 0; i < J; ++i) acc = pfma(splat2(L[j * J + i]), v[i], acc);
+        f32x2* o = reinterpret_cast<f32x2*>(dst + (p * J + j) * LDX + c);
         if (RESID) {
-            const float2 x = *o;
-            *o = make_float2(x.x + (a0 + b0), x.y + (a1 + b1));
+            *o = *o + (acc + bb);
         } else {
-            *o = make_float2(a0, a1);
+            *o = acc;
         }
     }
 }
@@ -724,11 +952,12 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
 #pragma unroll 1
     for (int s = 0; s < K; ++s) {
         // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
-        input_prep<SPARSE>(CW, XST, B1, tid);
-        __syncthreads();
         {
+            const auto pre = gemm_prefetch<6, 1>(W + OFF_WIN, wave, lane);
+            input_prep<SPARSE>(CW, XST, B1, tid);
+            __syncthreads();
             const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1};
-            gemm_wg<6, 1, 0, E_STORE>(B1, LDX, nullptr, 0, W + OFF_WIN, wave, lane, e);
+            gemm_wg<6, 1, 0, E_STORE>(B1, LDX, nullptr, 0, W + OFF_WIN, wave, lane, e, pre);
         }
         __syncthreads();
 
@@ -736,56 +965,75 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
         for (int l = 0; l < NL; ++l) {
             const float* LW = W + l * LAYER_FLOATS;
             // ---- x = x + MHA(LN0(x))   (GraAttenLayer, GraFormer.py:94-95)
-            if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
-            __syncthreads();
-            if (DPK_RUN(16 | 32)) {
-                const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
-                gemm_wg<18, 6, 0, E_STORE>(B1, LDX, nullptr, 0, LW + OFF_QKV, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
+                if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
+                __syncthreads();
+                if (DPK_RUN(16 | 32)) {
+                    const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg<18, 6, 0, E_STORE>(B1, LDX, nullptr, 0, LW + OFF_QKV, wave, lane, e, pre);
+                }
             }
             __syncthreads();
-            if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
-            __syncthreads();
-            if (DPK_RUN(16 | 64)) {
-                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
-                gemm_wg<6, 6, 0, E_RESID>(B1, LDX, nullptr, 0, LW + OFF_O, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
+                if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
+                __syncthreads();
+                if (DPK_RUN(16 | 64)) {
+                    const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg<6, 6, 0, E_RESID>(B1, LDX, nullptr, 0, LW + OFF_O, wave, lane, e, pre);
+                }
             }
             __syncthreads();
             // ---- x = x + GraphNet(LN1(x)) = x + L (relu((L LN1(x)) W1^T + b1) W2^T) + b2
             //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
-            if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
-            __syncthreads();
-            if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
-            __syncthreads();
-            if (DPK_RUN(16 | 128)) {
-                const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
-                gemm_wg<12, 6, 0, E_STORE_RELU>(B1, LDX, nullptr, 0, LW + OFF_FC1, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
+                if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
+                __syncthreads();
+                if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
+                __syncthreads();
+                if (DPK_RUN(16 | 128)) {
+                    const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg<12, 6, 0, E_STORE_RELU>(B1, LDX, nullptr, 0, LW + OFF_FC1, wave, lane, e, pre);
+                }
             }
-            __syncthreads();
-            if (DPK_RUN(16 | 256)) {
-                const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
-                gemm_wg<6, 12, 0, E_STORE_NB>(B2, LD2, nullptr, 0, LW + OFF_FC2, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
+                __syncthreads();
+                if (DPK_RUN(16 | 256)) {
+                    const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg<6, 12, 0, E_STORE_NB>(B2, LD2, nullptr, 0, LW + OFF_FC2, wave, lane, e, pre);
+                }
             }
-            __syncthreads();
-            if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
-            __syncthreads();
-            // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
-            if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
-            __syncthreads();
-            if (DPK_RUN(16 | 512)) {
-                const float* tp = a.tproj + (EPS_MODE ? 0 : (size_t)s * NL * D) + l * D;
-                const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
-                gemm_wg<6, 6, 12, E_CHEB1>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
+                __syncthreads();
+                if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
+                __syncthreads();
+                // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
+                if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
+                __syncthreads();
+                if (DPK_RUN(16 | 512)) {
+                    const float* tp = a.tproj + (EPS_MODE ? 0 : (size_t)s * NL * D) + l * D;
+                    const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
+                    gemm_wg<6, 6, 12, E_CHEB1>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, e, pre);
+                }
             }
-            __syncthreads();
-            if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
-            __syncthreads();
-            if (DPK_RUN(16 | 1024)) {
-                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
-                gemm_wg<6, 6, 12, E_RESID_RELU>(B1, LDX, B2, LD2, LW + OFF_C2, wave, lane, e);
+            {
+                const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
+                __syncthreads();
+                if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
+                __syncthreads();
+                if (DPK_RUN(16 | 1024)) {
+                    const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg<6, 6, 12, E_RESID_RELU>(B1, LDX, B2, LD2, LW + OFF_C2, wave, lane, e, pre);
+                }
             }
             __syncthreads();
         }
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
+        const auto preo = out_prefetch<18>(W + OFF_WOUT, lane);
         cheb_prep<SPARSE>(CW, XS, B2, tid);
         __syncthreads();
         {
@@ -811,8 +1059,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
                     }
                 }
             };
-            gemm_out<1, 6, 12>(XS, LDX, B2, LD2, Bo, wave, lane, epi);
-            if (wave == 3) gemm_out<1, 6, 12>(XS, LDX, B2, LD2, Bo, 4, lane, epi);
+            gemm_out<6, 12>(XS, LDX, B2, LD2, Bo, wave, lane, epi, preo);
         }
         __syncthreads();
     }

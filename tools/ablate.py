@@ -21,14 +21,22 @@ EXTRA = os.environ.get("DPK_ABLATE_EXTRA", "")
 
 
 def build():
+    from concurrent.futures import ThreadPoolExecutor
+
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_kernels.hip")
-    for m in MASKS:
+
+    def one(m):
         so = os.path.join(OUT, f"libdpk_a{m}.so")
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-ffp-contract=off", f"-I{ROOT}/include", f"-DDPK_ABLATE={m}", src, "-o", so] + EXTRA.split()
-        subprocess.run(cmd, check=True)
-        print("built", so)
+               "-ffp-contract=off", "-Wno-unused-result", f"-I{ROOT}/include", f"-DDPK_ABLATE={m}", src,
+               "-o", so] + EXTRA.split()
+        subprocess.run(cmd, check=True, capture_output=True)
+        return so
+
+    with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 1)) as ex:
+        for so in ex.map(one, MASKS):
+            print("built", so)
 
 
 def time_one(reps=5):
