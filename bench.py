@@ -77,14 +77,13 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from diffpose_amd import dist as D
     from diffpose_amd.data import repeat_hypotheses, shard_frames, synthetic_batch
     from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
     from diffpose_amd.schedule import get_beta_schedule, make_seq
     from diffpose_amd.weights import synthetic_state_dict
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = D.world_info()
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
@@ -108,12 +107,11 @@ def main():
     x = torch.from_numpy(x_host).to(dev)
     out = torch.empty_like(x)
     rows = x.shape[0]
-    gathered = torch.empty((world * rows, 17, 5), dtype=x.dtype, device=dev) if world > 1 else None
 
     def step():
         model.sample(x, seq, betas, eta=args.eta, out=out)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        if world > 1:                            # the one data-path collective: final poses to every rank
+            D.gather_frames(out, B_total, args.hyp)
 
     for _ in range(args.warmup):
         step()
@@ -145,11 +143,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
     kernel_ms = model.kernel_times_ms() if graph is None else []
     model.profile(False)
 

@@ -1,0 +1,114 @@
+"""CPU, world_size 2 over gloo: the frame-sharded multi-GPU path (diffpose_amd.dist), as
+bench.py runs it, with the golden-pinned oracle standing in for the per-rank sampler.
+
+Checks: every rank's shard + the all-gather reassembles the reference's hypothesis-major
+batch exactly (ragged and even shards, H>1), the metric all-reduce equals the
+single-process metric, and max-over-ranks timing.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_sampler():
+    from oracle import gcndiff_oracle as O
+    from diffpose_amd.schedule import get_beta_schedule, make_seq
+    from diffpose_amd.weights import synthetic_state_dict
+
+    P = O.params_to_torch(synthetic_state_dict())
+    adj = O.adjacency()
+    seq = make_seq("uniform", 50, 2)
+    b = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3, num_diffusion_timesteps=51)).float()
+    mask = torch.ones(1, 1, 17, dtype=torch.bool)
+
+    def run(x):
+        # one pose at a time: per-pose results must not depend on how frames are batched
+        outs = [O.generalized_steps(x[i:i + 1], mask, seq, lambda a, m, t: O.gcndiff_forward(P, adj, a, m, t), b)[0][-1]
+                for i in range(x.shape[0])]
+        return torch.cat(outs) if outs else x.clone()
+
+    return run
+
+
+def _worker(rank, port, n_frames, hyp, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "diffpose-nw_amd"), root):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    torch.set_num_threads(1)
+    try:
+        from diffpose_amd import dist as D
+        from diffpose_amd.data import repeat_hypotheses, shard_frames, synthetic_batch
+
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        x_all, tgt = synthetic_batch(n_frames, seed=31)
+        lo, hi = shard_frames(n_frames, WORLD, rank)
+        x_local = torch.from_numpy(repeat_hypotheses(x_all[lo:hi], hyp))
+        rows = D.shard_rows(n_frames, hyp, WORLD, rank)
+        assert torch.equal(x_local, torch.from_numpy(repeat_hypotheses(x_all, hyp))[rows])
+        out_local = _oracle_sampler()(x_local)
+        full = D.gather_frames(out_local, n_frames, hyp)
+        # metric numerators on the local frames (hypothesis mean is local)
+        o = out_local.double().view(hyp, hi - lo, 17, 5).mean(0)[:, :, 2:]
+        t = torch.from_numpy(tgt[lo:hi]).double()
+        err = torch.norm(o - o[:, :1] - t, dim=-1).mean(-1)
+        sums = D.allreduce_sums([float(err.sum()), float(hi - lo)])
+        tmax = D.max_over_ranks(float(rank + 1))
+        q.put((rank, full.numpy(), sums.numpy(), tmax))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, repr(e), None, None))
+        raise
+
+
+@pytest.mark.parametrize("n_frames,hyp", [(8, 1), (7, 2), (1, 3)])
+def test_sharded_sampling_matches_single_process(n_frames, hyp):
+    from diffpose_amd.data import repeat_hypotheses, synthetic_batch
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, n_frames, hyp, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(WORLD):
+            r, full, sums, tmax = q.get(timeout=300)
+            assert sums is not None, f"rank {r} failed: {full}"
+            res[r] = (full, sums, tmax)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+
+    x_all, tgt = synthetic_batch(n_frames, seed=31)
+    ref = _oracle_sampler()(torch.from_numpy(repeat_hypotheses(x_all, hyp))).numpy()
+    o = ref.astype(np.float64).reshape(hyp, n_frames, 17, 5).mean(0)[:, :, 2:]
+    ref_err = np.linalg.norm(o - o[:, :1] - tgt.astype(np.float64), axis=-1).mean(-1)
+    for r in range(WORLD):
+        full, sums, tmax = res[r]
+        assert np.array_equal(full, ref), f"rank {r}: gathered batch differs"
+        assert sums[1] == n_frames
+        assert abs(sums[0] - ref_err.sum()) <= 1e-12 * max(1.0, ref_err.sum())
+        assert tmax == float(WORLD)
