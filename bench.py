@@ -156,7 +156,7 @@ def main():
         achieved = W_ALG * rows * K / (avg_kernel_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_MFMA, 4), "traffic": None,
-                "kernel": "dpk::sample_kernel<false, *>", "avg_launch_ms": round(avg_kernel_ms, 4),
+                "kernel": "dpk::sample_kernel<0, *>", "avg_launch_ms": round(avg_kernel_ms, 4),
                 "launches": len(kernel_ms), "flop_per_launch": W_ALG * rows * K,
                 "per_unit": f"{W_ALG} FLOP per pose-step (SURVEY 8d) x {rows} poses x {K} steps"}
         tfile = os.path.join(ROOT, "profiles", "traffic.json")

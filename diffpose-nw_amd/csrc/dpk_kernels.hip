@@ -115,16 +115,26 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
 
+// Kernel modes: the K-step sampler (GCNdiff + DDIM), one GCNdiff eps evaluation, or one
+// GCNpose forward (models/gcnpose.py:101-113: the same backbone without the timestep
+// embedding, coords 2 -> 3), which also builds the sampler's uvxyz input
+// (runners/diffpose_frame.py:337-342).
+enum { M_SAMPLE = 0, M_EPS = 1, M_POSE = 2 };
+constexpr int CIN_POSE = 2, COUT_POSE = 3;
+
 struct SampleArgs {
     const float* arena;   // packed weights
     const float* coef;    // [K][6] = sqrt(1-at), sqrt(at), sqrt(an), c1, c2, t
-    const float* tproj;   // [slots][NL][D] temb_proj(swish(temb)) per step (sample) or per pose (eps)
-    const float* x_in;    // [N][17][5]
-    float* x_out;         // [N][17][5]  final x (sample) or eps (eps mode)
+    const float* tproj;   // [slots][NL][D] temb_proj(swish(temb)) per step (sample) / per pose (eps); zeros (pose)
+    const float* x_in;    // [N][17][5]  (pose: [N][17][2] uv)
+    float* x_out;         // [N][17][5]  final x (sample) or eps (eps mode); pose: [N][17][3] xyz or null
     float* xs;            // [K+1][N][17][5] or null
     float* x0s;           // [K][N][17][5]   or null
+    float* uvxyz;         // pose: [H][N][17][5] cat(uv, root-processed xyz), repeated H times; or null
     int N;
     int K;
+    int H;                // pose: test_times
+    int root_mode;        // pose: 0 reference in-place quirk (root zeroed), 1 root-relative, 2 raw
     unsigned mask;        // 17-bit key mask
     float eta;
     unsigned long long seed;
@@ -928,9 +938,12 @@ __device__ __forceinline__ void input_prep(const float* __restrict__ cw, const f
 }
 
 // ---------------------------------------------------------------------------------------
-// The sampler: K DDIM steps (or one eps evaluation) for P poses per workgroup.
-template <bool EPS_MODE, bool SPARSE>
+// The sampler: K DDIM steps (or one eps evaluation, or one GCNpose forward) for P poses
+// per workgroup.
+template <int MODE, bool SPARSE>
 __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
+    constexpr bool EPS_MODE = MODE == M_EPS;
+    constexpr bool POSE = MODE == M_POSE;
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
     float* XS = sm + SM_XS;
     float* B1 = sm + SM_B1;
@@ -945,10 +958,18 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
     const float* W = a.arena;
     const float* CW = W + (SPARSE ? OFF_CHEBS : OFF_CHEB);
 
-    for (int i = tid; i < R * CIN; i += NT) XST[i] = i < nvalid ? a.x_in[(size_t)pose0 * PE + i] : 0.f;
+    if constexpr (POSE) {
+        // uv into channels 0-1 of the 5-channel tile; the packed input weight is zero for 2-4
+        for (int i = tid; i < R * CIN; i += NT) {
+            const int row = i / CIN, c = i - row * CIN;
+            XST[i] = (c < CIN_POSE && row < npose * J) ? a.x_in[((size_t)pose0 * J + row) * CIN_POSE + c] : 0.f;
+        }
+    } else {
+        for (int i = tid; i < R * CIN; i += NT) XST[i] = i < nvalid ? a.x_in[(size_t)pose0 * PE + i] : 0.f;
+    }
     __syncthreads();
 
-    const int K = EPS_MODE ? 1 : a.K;
+    const int K = MODE == M_SAMPLE ? a.K : 1;
 #pragma unroll 1
     for (int s = 0; s < K; ++s) {
         // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
@@ -1015,7 +1036,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
                 if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
                 __syncthreads();
                 if (DPK_RUN(16 | 512)) {
-                    const float* tp = a.tproj + (EPS_MODE ? 0 : (size_t)s * NL * D) + l * D;
+                    const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
                     const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
                     gemm_wg<6, 6, 12, E_CHEB1>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, e, pre);
                 }
@@ -1033,20 +1054,27 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
             __syncthreads();
         }
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
+        //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly)
         const auto preo = out_prefetch<18>(W + OFF_WOUT, lane);
         cheb_prep<SPARSE>(CW, XS, B2, tid);
         __syncthreads();
         {
             const f32x4* Bo = reinterpret_cast<const f32x4*>(W + OFF_WOUT);
-            const float* cfp = a.coef + (EPS_MODE ? 0 : s * 6);
-            const float cf[5] = {cfp[0], cfp[1], cfp[2], cfp[3], cfp[4]};   // uniform: SGPRs
+            float cf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if constexpr (MODE == M_SAMPLE) {
+                const float* cfp = a.coef + s * 6;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) cf[i] = cfp[i];                  // uniform: SGPRs
+            }
             const float bo = W[OFF_BOUT + (lane & 15)];
             auto epi = [&](int r, int c, float v) {
                 const float et = v + bo;
                 const int idx = r * CIN + c;           // same as r*COUT+c (coords 5 -> 5)
                 const bool valid = idx < nvalid;
                 const size_t gidx = (size_t)pose0 * PE + idx;
-                if (EPS_MODE) {
+                if (POSE) {
+                    B1[r * LDX + c] = et;
+                } else if (EPS_MODE) {
                     if (valid) a.x_out[gidx] = et;
                 } else {
                     const float z = a.eta != 0.f ? normal_noise(a.seed, s, (long long)gidx) : 0.f;
@@ -1063,8 +1091,33 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
         }
         __syncthreads();
     }
-    if (!EPS_MODE)
+    if constexpr (MODE == M_SAMPLE) {
         for (int i = tid; i < nvalid; i += NT) a.x_out[(size_t)pose0 * PE + i] = XST[i];
+    } else if constexpr (POSE) {
+        // inputs_xyz = model_pose(input_2d); inputs_xyz -= root; input_uvxyz = cat(uv, xyz).repeat(H)
+        // (runners/diffpose_frame.py:337-342).  root_mode 0 = what the reference's aliased in-place
+        // `x[:, :, :] -= x[:, :1, :]` yields on CPU torch (only the root row is zeroed).
+        if (a.x_out)
+            for (int i = tid; i < npose * J * COUT_POSE; i += NT) {
+                const int row = i / COUT_POSE, c = i - row * COUT_POSE;
+                a.x_out[(size_t)pose0 * J * COUT_POSE + i] = B1[row * LDX + c];
+            }
+        if (a.uvxyz)
+            for (int i = tid; i < npose * PE; i += NT) {
+                const int row = i / CIN, c = i - row * CIN;
+                float v;
+                if (c < CIN_POSE) {
+                    v = XST[i];
+                } else {
+                    const float raw = B1[row * LDX + (c - CIN_POSE)];
+                    const int j = row % J;
+                    if (a.root_mode == 0) v = j == 0 ? 0.f : raw;
+                    else if (a.root_mode == 1) v = raw - B1[(row - j) * LDX + (c - CIN_POSE)];
+                    else v = raw;
+                }
+                for (int hh = 0; hh < a.H; ++hh) a.uvxyz[((size_t)hh * a.N + pose0) * PE + i] = v;
+            }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1132,6 +1185,7 @@ using namespace dpk;
 
 struct dpk_handle {
     int device = 0;
+    int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
@@ -1226,6 +1280,15 @@ static void graph_lap(const float* A, float* Lg) {
         for (int j = 0; j < J; ++j) Lg[i * J + j] = (dh[i] * A[i * J + j]) * dh[j];
 }
 
+static int ensure_tproj(dpk_handle* h, int slots) {
+    if (h->tproj_cap >= slots) return DPK_OK;
+    if (h->tproj) HIPCHK(h, hipFree(h->tproj));
+    h->tproj = nullptr;
+    HIPCHK(h, hipMalloc(&h->tproj, (size_t)slots * NL * D * 4));
+    h->tproj_cap = slots;
+    return DPK_OK;
+}
+
 static int upload(dpk_handle* h) {
     HIPCHK(h, hipSetDevice(h->device));
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
@@ -1249,13 +1312,17 @@ int dpk_kernel_geometry(int* ppw, int* tpw, int* lds) {
 int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (!cfg || !out) return DPK_E_INVALID;
     *out = nullptr;
-    if (cfg->hid_dim != D || cfg->num_layers != NL || cfg->n_head != NH || cfg->n_pts != J ||
-        cfg->coords_in != CIN || cfg->coords_out != COUT)
+    if (cfg->hid_dim != D || cfg->num_layers != NL || cfg->n_head != NH || cfg->n_pts != J)
         return DPK_E_UNSUPPORTED;
+    int kind;
+    if (cfg->coords_in == CIN && cfg->coords_out == COUT) kind = 0;
+    else if (cfg->coords_in == CIN_POSE && cfg->coords_out == COUT_POSE) kind = 1;
+    else return DPK_E_UNSUPPORTED;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return DPK_E_HIP;
     dpk_handle* h = new dpk_handle();
     h->device = cfg->device;
+    h->kind = kind;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_temb.assign(TEMB_FLOATS, 0.f);
     *out = h;
@@ -1344,6 +1411,8 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
     const float* var = get(key, numel);                                  \
     if (!var) return fail(h, DPK_E_WEIGHTS, "dpk_load_weights: " + missing);
 
+    const bool pose = h->kind == 1;
+    const int cin = pose ? CIN_POSE : CIN, cout = pose ? COUT_POSE : COUT;
     float* A = h->h_arena.data();
     for (int l = 0; l < NL; ++l) {
         float* Lw = A + (size_t)l * LAYER_FLOATS;
@@ -1370,8 +1439,14 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         GET(c1b, gc + "gconv1.gconv.bias", D);
         GET(c2w, gc + "gconv2.gconv.weight", 3 * D * D);
         GET(c2b, gc + "gconv2.gconv.bias", D);
-        GET(tpw, gc + "temb_proj.weight", D * E);
-        GET(tpb, gc + "temb_proj.bias", D);
+        const float* tpw = nullptr;
+        const float* tpb = nullptr;
+        if (!pose) {     // GCNpose's _ResChebGC has no temb_proj (models/ChebConv.py:154-165)
+            GET(tpw_, gc + "temb_proj.weight", D * E);
+            GET(tpb_, gc + "temb_proj.bias", D);
+            tpw = tpw_;
+            tpb = tpb_;
+        }
         // nn.Linear weight is (out, in): W_eff[k][n] = weight[n][k]
         pack_blocks(Lw + OFF_QKV, D, D3, KB_D, 18, [&](int k, int n) {
             const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
@@ -1399,39 +1474,54 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         for (int c = 0; c < D2; ++c) Lw[OFF_BFC1 + c] = f1b[c];
         graph_lap(ahat, Lw + OFF_LG);
         // temb_proj: transposed [in=384][out=96]
-        float* T = h->h_temb.data();
-        for (int o = 0; o < D; ++o) {
-            for (int k = 0; k < E; ++k) T[TOFF_WP + (size_t)l * E * D + k * D + o] = tpw[o * E + k];
-            T[TOFF_BP + l * D + o] = tpb[o];
+        if (!pose) {
+            float* T = h->h_temb.data();
+            for (int o = 0; o < D; ++o) {
+                for (int k = 0; k < E; ++k) T[TOFF_WP + (size_t)l * E * D + k * D + o] = tpw[o * E + k];
+                T[TOFF_BP + l * D + o] = tpb[o];
+            }
         }
     }
-    GET(wi, "gconv_input.weight", 3 * CIN * D);
+    GET(wi, "gconv_input.weight", 3 * cin * D);
     GET(bi, "gconv_input.bias", D);
-    GET(wout, "gconv_output.weight", 3 * D * COUT);
-    GET(bout, "gconv_output.bias", COUT);
-    GET(d0w, "temb.dense.0.weight", E * D);
-    GET(d0b, "temb.dense.0.bias", E);
-    GET(d1w, "temb.dense.1.weight", E * E);
-    GET(d1b, "temb.dense.1.bias", E);
-#undef GET
-    pack_blocks(A + OFF_WIN, 3 * CIN, D, 1, 6, [&](int k, int n) { return wi[(k / CIN) * CIN * D + (k % CIN) * D + n]; });
-    pack_blocks(A + OFF_WOUT, D3, COUT, KB_D3, 1,
-                [&](int k, int n) { return wout[(k / D) * D * COUT + (k % D) * COUT + n]; });
+    GET(wout, "gconv_output.weight", 3 * D * cout);
+    GET(bout, "gconv_output.bias", cout);
+    // input rows k = order*5 + channel of the 5-channel tile; GCNpose's channels 2-4 are zero
+    pack_blocks(A + OFF_WIN, 3 * CIN, D, 1, 6, [&](int k, int n) {
+        const int o = k / CIN, c = k % CIN;
+        return c < cin ? wi[o * cin * D + c * D + n] : 0.f;
+    });
+    pack_blocks(A + OFF_WOUT, D3, cout, KB_D3, 1,
+                [&](int k, int n) { return wout[(k / D) * D * cout + (k % D) * cout + n]; });
     for (int c = 0; c < D; ++c) A[OFF_BIN + c] = bi[c];
-    for (int c = 0; c < 16; ++c) A[OFF_BOUT + c] = c < COUT ? bout[c] : 0.f;
-    float* T = h->h_temb.data();
-    for (int o = 0; o < E; ++o) {
-        for (int k = 0; k < D; ++k) T[TOFF_W0 + k * E + o] = d0w[o * D + k];
-        for (int k = 0; k < E; ++k) T[TOFF_W1 + k * E + o] = d1w[o * E + k];
-        T[TOFF_B0 + o] = d0b[o];
-        T[TOFF_B1 + o] = d1b[o];
+    for (int c = 0; c < 16; ++c) A[OFF_BOUT + c] = c < cout ? bout[c] : 0.f;
+    if (!pose) {         // GCNpose carries temb.dense too (gcnpose.py:94-98) but never uses it
+        GET(d0w, "temb.dense.0.weight", E * D);
+        GET(d0b, "temb.dense.0.bias", E);
+        GET(d1w, "temb.dense.1.weight", E * E);
+        GET(d1b, "temb.dense.1.bias", E);
+        float* T = h->h_temb.data();
+        for (int o = 0; o < E; ++o) {
+            for (int k = 0; k < D; ++k) T[TOFF_W0 + k * E + o] = d0w[o * D + k];
+            for (int k = 0; k < E; ++k) T[TOFF_W1 + k * E + o] = d1w[o * E + k];
+            T[TOFF_B0 + o] = d0b[o];
+            T[TOFF_B1 + o] = d1b[o];
+        }
     }
+#undef GET
     h->have_weights = true;
-    return upload(h);
+    int rc = upload(h);
+    if (rc || !pose) return rc;
+    // the pose backbone adds no timestep projection: a zero row per layer (E_CHEB1 adds +0)
+    rc = ensure_tproj(h, 1);
+    if (rc) return rc;
+    HIPCHK(h, hipMemset(h->tproj, 0, (size_t)NL * D * 4));
+    return DPK_OK;
 }
 
 int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* seq, int K, float eta) {
     if (!h || !abar || !seq || K <= 0 || n_alpha < 2) return fail(h, DPK_E_INVALID, "dpk_set_schedule: bad args");
+    if (h->kind != 0) return fail(h, DPK_E_STATE, "GCNpose handle (coords 2->3) has no diffusion schedule");
     std::vector<float> c((size_t)K * 6);
     // execution order: i over reversed(seq), j over reversed([-1] + seq[:-1]) (utils_diff.py:49-52)
     for (int s = 0; s < K; ++s) {
@@ -1473,16 +1563,11 @@ int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* s
     return DPK_OK;
 }
 
-static int ensure_tproj(dpk_handle* h, int slots) {
-    if (h->tproj_cap >= slots) return DPK_OK;
-    if (h->tproj) HIPCHK(h, hipFree(h->tproj));
-    h->tproj = nullptr;
-    HIPCHK(h, hipMalloc(&h->tproj, (size_t)slots * NL * D * 4));
-    h->tproj_cap = slots;
-    return DPK_OK;
-}
 
-static int check_ready(dpk_handle* h) {
+static int check_ready(dpk_handle* h, int kind = 0) {
+    if (h->kind != kind)
+        return fail(h, DPK_E_STATE, kind ? "GCNdiff handle: dpk_pose needs a GCNpose handle (coords 2->3)"
+                                         : "GCNpose handle (coords 2->3): use dpk_pose");
     if (!h->have_graph) return fail(h, DPK_E_STATE, "graph (adjacency) not set");
     if (!h->have_weights) return fail(h, DPK_E_STATE, "weights not loaded");
     return DPK_OK;
@@ -1512,9 +1597,9 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<true, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_EPS, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     else
-        hipLaunchKernelGGL((sample_kernel<true, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_EPS, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -1551,11 +1636,43 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<false, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     else
-        hipLaunchKernelGGL((sample_kernel<false, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
+    return DPK_OK;
+}
+
+int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, int H, int root_mode,
+             void* stream) {
+    if (!h) return DPK_E_INVALID;
+    if (N < 0 || H < 1 || root_mode < 0 || root_mode > 2 || (N > 0 && (!x2d || (!xyz && !uvxyz))))
+        return fail(h, DPK_E_INVALID, "dpk_pose: bad args");
+    int rc = check_ready(h, 1);
+    if (rc) return rc;
+    if (N == 0) return DPK_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    SampleArgs a{};
+    a.arena = h->arena;
+    a.tproj = h->tproj;   // zeros
+    a.x_in = x2d;
+    a.x_out = xyz;
+    a.uvxyz = uvxyz;
+    a.N = N;
+    a.K = 1;
+    a.H = H;
+    a.root_mode = root_mode;
+    a.mask = h->mask;
+    std::pair<hipEvent_t, hipEvent_t> ev;
+    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
+    if (h->sparse_graph)
+        hipLaunchKernelGGL((sample_kernel<M_POSE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    else
+        hipLaunchKernelGGL((sample_kernel<M_POSE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+    HIPCHK(h, hipGetLastError());
+    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;
 }
 

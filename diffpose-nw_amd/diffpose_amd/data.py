@@ -39,3 +39,16 @@ def shard_frames(n_frames: int, world: int, rank: int):
 def repeat_hypotheses(x: np.ndarray, test_times: int) -> np.ndarray:
     """``input_uvxyz.repeat(test_times,1,1)`` — hypothesis-major rows (diffpose_frame.py:342)."""
     return np.ascontiguousarray(np.tile(x, (test_times, 1, 1)))
+
+
+def synthetic_eval_batches(n_frames: int, batch_size: int, seed: int = DEFAULT_SEED):
+    """Yield (input_2d [B,17,2], targets_3d [B,17,3], actions [B]) like test_hyber's loader
+    (runners/diffpose_frame.py:278-283, shuffle=False, so frames arrive grouped by action and
+    most batches hold a single action string; batches at a boundary mix two)."""
+    from .metrics import TEST_ACTIONS
+
+    x, tgt = synthetic_batch(n_frames, seed=seed)
+    acts = np.array([f"{TEST_ACTIONS[(f * len(TEST_ACTIONS)) // max(n_frames, 1)]} 1" for f in range(n_frames)])
+    for lo in range(0, n_frames, batch_size):
+        hi = min(lo + batch_size, n_frames)
+        yield np.ascontiguousarray(x[lo:hi, :, :2]), tgt[lo:hi], [str(a) for a in acts[lo:hi]]

@@ -48,18 +48,21 @@ def _dev_index(device) -> int:
     return torch.cuda.current_device() if d.index is None else d.index
 
 
-def _model_dims(config):
+def _model_dims(config, default_coords=COORDS):
     if config is None:
-        return HID, N_LAYERS, N_HEAD, N_PTS, tuple(COORDS)
+        return HID, N_LAYERS, N_HEAD, N_PTS, tuple(default_coords)
     m = getattr(config, "model", config)
     return (int(m.hid_dim), int(m.num_layer), int(m.n_head), int(m.n_pts), tuple(int(c) for c in m.coords_dim))
 
 
-class HipGCNdiff:
-    """GCNdiff(adj, config) on MI355X.  ``model(x, mask, t, cemd) -> eps`` like the reference."""
+class _HipModel:
+    """A libdpk handle for one model (graph, weights, key mask) on one HIP device."""
+
+    KIND = "diff"
+    DEFAULT_COORDS = COORDS
 
     def __init__(self, adj, config=None, device=None):
-        hid, nl, nh, npts, coords = _model_dims(config)
+        hid, nl, nh, npts, coords = _model_dims(config, self.DEFAULT_COORDS)
         self.device = torch.device("cuda", _dev_index(device))
         L = _lib.lib()
         cfg = _lib.DpkConfig(hid, nl, nh, npts, coords[0], coords[1], self.device.index)
@@ -80,7 +83,7 @@ class HipGCNdiff:
     # -- nn.Module-like surface -------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True):
         """Accept the reference's states[0] (with/without 'module.'), torch tensors or numpy."""
-        sd = normalize_state_dict(state_dict)
+        sd = normalize_state_dict(state_dict, kind=self.KIND)
         names = list(sd.keys())
         arrs = [np.ascontiguousarray(sd[k], dtype=np.float32) for k in names]
         c_names = (ctypes.c_char_p * len(names))(*[k.encode() for k in names])
@@ -97,7 +100,8 @@ class HipGCNdiff:
 
     def train(self, mode: bool = True):
         if mode:
-            raise NotImplementedError("HipGCNdiff is inference-only (training is out of scope, SURVEY §8f f4)")
+            raise NotImplementedError(f"{type(self).__name__} is inference-only (training is out of scope, "
+                                      "SURVEY §8f f4)")
         return self.eval()
 
     def to(self, *a, **k):
@@ -130,6 +134,43 @@ class HipGCNdiff:
             self.set_mask(mask)
             self._mask_key = key
 
+    def _check_x(self, x, channels: int = 5):
+        if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32):
+            raise TypeError("x must be a float32 CUDA(HIP) tensor")
+        if x.dim() != 3 or x.shape[1] != self.n_pts or x.shape[2] != channels:
+            raise ValueError(f"x must be (N, {self.n_pts}, {channels}), got {tuple(x.shape)}")
+        if x.device != self.device:
+            raise ValueError(f"x on {x.device}, model on {self.device}")
+        return x.contiguous()
+
+    def profile(self, enable: bool = True) -> None:
+        """Bracket each model-kernel launch with HIP events (see dpk_profile)."""
+        _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))
+
+    def kernel_times_ms(self):
+        """Wait for and return the recorded kernel durations (ms), oldest first."""
+        L = _lib.lib()
+        cap = 4096
+        buf = (ctypes.c_float * cap)()
+        n = ctypes.c_int()
+        _lib.check(self._h, "dpk_profile_read", L.dpk_profile_read(self._h, buf, cap, ctypes.byref(n)))
+        return [buf[i] for i in range(min(n.value, cap))]
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            _lib.lib().dpk_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HipGCNdiff(_HipModel):
+    """GCNdiff(adj, config) on MI355X.  ``model(x, mask, t, cemd) -> eps`` like the reference."""
+
     # -- schedule -------------------------------------------------------------------
     def set_schedule(self, seq, betas, eta: float = 0.0) -> None:
         """Bind seq / betas / eta (cached: re-uploaded only when they change)."""
@@ -148,15 +189,6 @@ class HipGCNdiff:
         self.K = len(seq)
 
     # -- compute --------------------------------------------------------------------
-    def _check_x(self, x):
-        if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32):
-            raise TypeError("x must be a float32 CUDA(HIP) tensor")
-        if x.dim() != 3 or x.shape[1] != self.n_pts or x.shape[2] != 5:
-            raise ValueError(f"x must be (N, {self.n_pts}, 5), got {tuple(x.shape)}")
-        if x.device != self.device:
-            raise ValueError(f"x on {x.device}, model on {self.device}")
-        return x.contiguous()
-
     def forward(self, x, mask, t, cemd=0):
         """eps = GCNdiff(x, mask, t) (models/gcndiff.py:101-113); ``cemd`` is unused there too."""
         x = self._check_x(x)
@@ -211,29 +243,6 @@ class HipGCNdiff:
         _lib.check(self._h, "dpk_ddim_update", rc)
         return xn, x0
 
-    def profile(self, enable: bool = True) -> None:
-        """Bracket each sampler-kernel launch with HIP events (see dpk_profile)."""
-        _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))
-
-    def kernel_times_ms(self):
-        """Wait for and return the recorded sampler-kernel durations (ms), oldest first."""
-        L = _lib.lib()
-        cap = 4096
-        buf = (ctypes.c_float * cap)()
-        n = ctypes.c_int()
-        _lib.check(self._h, "dpk_profile_read", L.dpk_profile_read(self._h, buf, cap, ctypes.byref(n)))
-        return [buf[i] for i in range(min(n.value, cap))]
-
-    def close(self):
-        h, self._h = getattr(self, "_h", None), None
-        if h:
-            _lib.lib().dpk_destroy(h)
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def GCNdiff(adj, config, device=None) -> HipGCNdiff:   # noqa: N802  (reference constructor name)

@@ -40,12 +40,21 @@ N_LAYERS = 5      # config.model.num_layer
 N_HEAD = 4        # config.model.n_head
 N_PTS = 17        # config.model.n_pts
 COORDS = (5, 5)   # config.model.coords_dim (uvxyz in, eps out)
+POSE_COORDS = (2, 3)  # GCNpose: uv in, xyz out (runners/diffpose_frame.py:138)
 DEFAULT_SEED = 19960903  # main_diffpose_frame.py:20
+POSE_SEED = DEFAULT_SEED + 1
 
 
 def param_shapes(hid: int = HID, n_layers: int = N_LAYERS, n_pts: int = N_PTS,
-                 coords=COORDS) -> "OrderedDict[str, tuple]":
-    """Ordered (key -> shape) of GCNdiff's state_dict (models/gcndiff.py:55-99)."""
+                 coords=None, kind: str = "diff") -> "OrderedDict[str, tuple]":
+    """Ordered (key -> shape) of GCNdiff's state_dict (models/gcndiff.py:55-99), or with
+    ``kind="pose"`` of GCNpose's (models/gcnpose.py:55-98: coords [2,3], no temb_proj in its
+    _ResChebGC blocks, the unused temb.dense layers still registered)."""
+    if kind not in ("diff", "pose"):
+        raise ValueError(f"kind must be 'diff' or 'pose', got {kind!r}")
+    pose = kind == "pose"
+    if coords is None:
+        coords = POSE_COORDS if pose else COORDS
     emb = 4 * hid
     s: "OrderedDict[str, tuple]" = OrderedDict()
     s["gconv_input.weight"] = (3, 1, coords[0], hid)
@@ -55,8 +64,9 @@ def param_shapes(hid: int = HID, n_layers: int = N_LAYERS, n_pts: int = N_PTS,
         for g in ("gconv1", "gconv2"):
             s[p + g + ".gconv.weight"] = (3, 1, hid, hid)
             s[p + g + ".gconv.bias"] = (1, 1, hid)
-        s[p + "temb_proj.weight"] = (hid, emb)
-        s[p + "temb_proj.bias"] = (hid,)
+        if not pose:
+            s[p + "temb_proj.weight"] = (hid, emb)
+            s[p + "temb_proj.bias"] = (hid,)
     for i in range(n_layers):
         p = f"atten_layers.{i}."
         for j in range(4):
@@ -101,8 +111,11 @@ def _draw(rng: np.random.Generator, key: str, shape: tuple) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
-def synthetic_state_dict(seed: int = DEFAULT_SEED, **shape_kw) -> "OrderedDict[str, np.ndarray]":
-    """Deterministic synthetic GCNdiff weights (float32 numpy arrays, no prefix)."""
+def synthetic_state_dict(seed: int | None = None, **shape_kw) -> "OrderedDict[str, np.ndarray]":
+    """Deterministic synthetic GCNdiff (or, ``kind="pose"``, GCNpose) weights (float32 numpy
+    arrays, no prefix).  Default seeds: DEFAULT_SEED (diff), POSE_SEED (pose)."""
+    if seed is None:
+        seed = POSE_SEED if shape_kw.get("kind") == "pose" else DEFAULT_SEED
     rng = np.random.Generator(np.random.PCG64(seed))
     shapes = param_shapes(**shape_kw)
     out: "OrderedDict[str, np.ndarray]" = OrderedDict()
@@ -116,10 +129,10 @@ def synthetic_state_dict(seed: int = DEFAULT_SEED, **shape_kw) -> "OrderedDict[s
     return out
 
 
-def state_dict_sha256(sd) -> str:
+def state_dict_sha256(sd, kind: str = "diff") -> str:
     """sha256 over key names and little-endian float32 payloads, in layout order."""
     h = hashlib.sha256()
-    for key in param_shapes():
+    for key in param_shapes(kind=kind):
         a = np.ascontiguousarray(np.asarray(sd[key], dtype="<f4"))
         h.update(key.encode())
         h.update(a.tobytes())
@@ -134,14 +147,14 @@ def strip_module_prefix(sd) -> "OrderedDict[str, object]":
     return out
 
 
-def normalize_state_dict(sd) -> "OrderedDict[str, np.ndarray]":
-    """Validate a GCNdiff state_dict against the layout; return float32 numpy arrays.
+def normalize_state_dict(sd, kind: str = "diff") -> "OrderedDict[str, np.ndarray]":
+    """Validate a GCNdiff (GCNpose) state_dict against the layout; return float32 numpy arrays.
 
     Raises KeyError for missing/unexpected keys and ValueError for shape
     mismatches, mirroring ``nn.Module.load_state_dict(strict=True)``.
     """
     sd = strip_module_prefix(sd)
-    shapes = param_shapes()
+    shapes = param_shapes(kind=kind)
     missing = [k for k in shapes if k not in sd]
     unexpected = [k for k in sd if k not in shapes]
     if missing or unexpected:
@@ -158,7 +171,7 @@ def normalize_state_dict(sd) -> "OrderedDict[str, np.ndarray]":
     return out
 
 
-def load_checkpoint(path: str) -> "OrderedDict[str, np.ndarray]":
+def load_checkpoint(path: str, kind: str = "diff") -> "OrderedDict[str, np.ndarray]":
     """Load a reference checkpoint (list with states[0] = model state_dict) safely.
 
     Uses ``torch.load(weights_only=True)`` — never unpickles arbitrary objects.
@@ -168,4 +181,4 @@ def load_checkpoint(path: str) -> "OrderedDict[str, np.ndarray]":
     states = torch.load(path, map_location="cpu", weights_only=True)
     if isinstance(states, (list, tuple)):
         states = states[0]
-    return normalize_state_dict(states)
+    return normalize_state_dict(states, kind=kind)

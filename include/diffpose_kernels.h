@@ -36,9 +36,10 @@ extern "C" {
 
 typedef struct dpk_handle dpk_handle;
 
-/* GCNdiff hyper-parameters (configs/human36m_diffpose_uvxyz_*.yml model: section,
+/* Model hyper-parameters (configs/human36m_diffpose_uvxyz_*.yml model: section,
  * emd_dim = 4*hid_dim per models/gcndiff.py:68).  The kernels are compiled for
- * hid_dim 96, num_layer 5, n_head 4, n_pts 17, coords_dim [5,5]. */
+ * hid_dim 96, num_layer 5, n_head 4, n_pts 17 and coords_dim [5,5] (GCNdiff, the
+ * denoiser) or [2,3] (GCNpose, the 2D->3D front-end; runners/diffpose_frame.py:138). */
 typedef struct {
     int hid_dim;
     int num_layers;
@@ -99,6 +100,33 @@ int dpk_sample(dpk_handle* h, const float* x_dev, float* out_dev, float* xs_dev,
  * (0 = first executed step, t = seq[K-1]).  x0_out may be NULL. */
 int dpk_ddim_update(dpk_handle* h, const float* xt_dev, const float* eps_dev, float* xnext_dev,
                     float* x0_dev, int64_t n_elems, int step, uint64_t seed, void* stream);
+
+/* GCNpose front-end (models/gcnpose.py:55-113) for a handle created with coords_in 2,
+ * coords_out 3 (create_pose_model, runners/diffpose_frame.py:134-154), fused with the
+ * sampler-input assembly of test_hyber (runners/diffpose_frame.py:337-342):
+ *   x2d_dev   [N,17,2]  input_2d
+ *   xyz_dev   [N,17,3]  model_pose(input_2d) as returned by the model, or NULL
+ *   uvxyz_dev [H,N,17,5] cat(input_2d, root-processed xyz).repeat(H,1,1), or NULL
+ *   root_mode 0: what the reference's in-place `xyz[:, :, :] -= xyz[:, :1, :]` yields on CPU
+ *                torch (aliasing: only the root row is zeroed; pinned by golden g5)
+ *             1: true root-relative (xyz - xyz[:, :1]);  2: no root subtraction
+ * The key mask of dpk_set_mask applies (GCNpose.forward(x, mask)).  At least one of
+ * xyz_dev / uvxyz_dev must be non-NULL. */
+int dpk_pose(dpk_handle* h, const float* x2d_dev, float* xyz_dev, float* uvxyz_dev, int N, int H,
+             int root_mode, void* stream);
+
+/* Per-frame evaluation of the sampler output (test_hyber, runners/diffpose_frame.py:382-387),
+ * handle-free, one thread per frame, fp64:
+ *   out_uvxyz_dev [H,F,17,5] sampler output (hypothesis-major, as generalized_steps returns it)
+ *   targets_dev   [F,17,3]   targets_3d
+ *   root_mode     as in dpk_pose, applied to prediction and target
+ *   p1_dev [F] (double)      MPJPE of each frame (metres; common/utils.py:103-127 per frame)
+ *   p2_dev [F] (double)      P-MPJPE of each frame, after the best similarity transform
+ *                            (common/loss.py:25-64 / common/utils.py:155-187)
+ *   xyz_dev [F,17,3] or NULL the hypothesis-mean, root-processed xyz (output_xyz)
+ * Returns DPK_OK, DPK_E_INVALID or DPK_E_HIP (no handle, so no dpk_last_error text). */
+int dpk_pose_metrics(const float* out_uvxyz_dev, const float* targets_dev, int F, int H, int root_mode,
+                     double* p1_dev, double* p2_dev, float* xyz_dev, void* stream);
 
 /* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /
  * dpk_eps brackets its sampler-kernel launch with a pair of HIP events on the

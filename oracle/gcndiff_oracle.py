@@ -18,6 +18,8 @@ What it restates (reference at /root/reference, file:line):
   ``GraAttenLayer`` GraFormer.py:84-96, ``SublayerConnection`` :73-81,
   ``_ResChebGC_diff`` gcndiff.py:39-53, ``_GraphConv`` ChebConv.py:133-151; eval mode,
   dropout = identity)
+* ``gcnpose_forward``  — ``GCNpose.forward``  models/gcnpose.py:101-113 (``_ResChebGC``
+  ChebConv.py:154-165); ``build_uvxyz`` — runners/diffpose_frame.py:337-342
 * ``generalized_steps`` — common/utils_diff.py:46-68
 * ``post_process`` / ``mpjpe`` — runners/diffpose_frame.py:382-386, common/loss.py:7-13
 
@@ -157,6 +159,43 @@ def gcndiff_forward(p: dict, graph: torch.Tensor, x: torch.Tensor, mask, t: torc
         h = F.relu(cheb_conv(h, graph, p[g + "gconv2.gconv.weight"], p[g + "gconv2.gconv.bias"]))
         out = out + h
     return cheb_conv(out, graph, p["gconv_output.weight"], p["gconv_output.bias"])
+
+
+def gcnpose_forward(p: dict, graph: torch.Tensor, x: torch.Tensor, mask, n_layers: int = 5,
+                    heads: int = 4) -> torch.Tensor:
+    """GCNpose.forward(x, mask) in eval mode (gcnpose.py:101-113): the GCNdiff backbone without
+    the timestep embedding; its blocks are ``_ResChebGC`` (ChebConv.py:154-165):
+    x + relu(Cheb2(relu(Cheb1(x))))."""
+    out = cheb_conv(x, graph, p["gconv_input.weight"], p["gconv_input.bias"])
+    for i in range(n_layers):
+        a = f"atten_layers.{i}."
+        lw = [p[a + f"self_attn.linears.{j}.weight"] for j in range(4)]
+        lb = [p[a + f"self_attn.linears.{j}.bias"] for j in range(4)]
+        y = layer_norm(out, p[a + "sublayer.0.norm.a_2"], p[a + "sublayer.0.norm.b_2"])
+        out = out + multi_head_attention(y, mask, lw, lb, heads)[0]
+        y = layer_norm(out, p[a + "sublayer.1.norm.a_2"], p[a + "sublayer.1.norm.b_2"])
+        out = out + graph_net(y, p[a + "feed_forward.A_hat"],
+                              p[a + "feed_forward.gconv1.fc.weight"], p[a + "feed_forward.gconv1.fc.bias"],
+                              p[a + "feed_forward.gconv2.fc.weight"], p[a + "feed_forward.gconv2.fc.bias"])
+        g = f"gconv_layers.{i}."
+        h = F.relu(cheb_conv(out, graph, p[g + "gconv1.gconv.weight"], p[g + "gconv1.gconv.bias"]))
+        h = F.relu(cheb_conv(h, graph, p[g + "gconv2.gconv.weight"], p[g + "gconv2.gconv.bias"]))
+        out = out + h
+    return cheb_conv(out, graph, p["gconv_output.weight"], p["gconv_output.bias"])
+
+
+def build_uvxyz(input_2d: torch.Tensor, xyz: torch.Tensor, test_times: int, root_mode: str = "quirk"):
+    """input_uvxyz of test_hyber (runners/diffpose_frame.py:337-342): root handling of the pose
+    output, cat with the 2D input, repeat(test_times, 1, 1).  root_mode "quirk" = what the
+    reference's in-place subtraction yields on CPU torch (root row zeroed only, golden g5);
+    "relative" = xyz - xyz[:, :1]; "raw" = unchanged."""
+    if root_mode == "quirk":
+        xyz = root_subtract_inplace_quirk(xyz)
+    elif root_mode == "relative":
+        xyz = xyz - xyz[:, :1, :].clone()
+    elif root_mode != "raw":
+        raise ValueError(root_mode)
+    return torch.cat([input_2d, xyz], dim=2).repeat(test_times, 1, 1)
 
 
 def alpha_at(b: torch.Tensor, t: torch.Tensor) -> torch.Tensor:

@@ -51,6 +51,15 @@ def test_argument_validation_without_gpu():
     assert L.dpk_create(ctypes.byref(bad), ctypes.byref(h)) == -2
     assert L.dpk_eps(None, None, None, None, 0, None) == -1
     assert L.dpk_last_error(None) == b"null handle"
+    bad_pose = _lib.DpkConfig(96, 5, 4, 17, 3, 3, 0)        # coords other than [5,5] / [2,3]
+    assert L.dpk_create(ctypes.byref(bad_pose), ctypes.byref(h)) == -2
+    assert L.dpk_pose(None, None, None, None, 0, 1, 0, None) == -1
+    # metrics entry validates before launching: negative F, H < 1, unknown root mode, null outputs
+    assert L.dpk_pose_metrics(None, None, -1, 1, 0, None, None, None, None) == -1
+    assert L.dpk_pose_metrics(None, None, 4, 0, 0, None, None, None, None) == -1
+    assert L.dpk_pose_metrics(None, None, 4, 1, 3, None, None, None, None) == -1
+    assert L.dpk_pose_metrics(None, None, 4, 1, 0, None, None, None, None) == -1
+    assert L.dpk_pose_metrics(None, None, 0, 1, 0, None, None, None, None) == 0
 
 
 def test_no_oracle_in_product_path():

@@ -183,3 +183,19 @@ def test_synthetic_data_and_sharding():
     assert all(spans[i][1] == spans[i + 1][0] for i in range(7))
     r = repeat_hypotheses(a[:4], 3)
     assert r.shape == (12, 17, 5) and np.array_equal(r[4:8], a[:4])
+
+
+def test_gcnpose_oracle(golden, graph):
+    """GCNpose front-end + test_hyber's uvxyz assembly (g6, from the reference GCNpose)."""
+    from diffpose_amd.weights import synthetic_state_dict, state_dict_sha256
+
+    g = golden("g6_gcnpose.npz")
+    sd = synthetic_state_dict(kind="pose")
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    assert state_dict_sha256(sd, kind="pose") == meta["pose_weights_sha256"]
+    P = O.params_to_torch(sd)
+    x2d = torch.from_numpy(g["x2d"])
+    xyz = O.gcnpose_forward(P, graph, x2d, torch.ones(1, 1, 17, dtype=torch.bool))
+    assert np.array_equal(xyz.numpy(), g["xyz"])
+    assert np.array_equal(O.gcnpose_forward(P, graph, x2d, torch.from_numpy(g["mask2"])).numpy(), g["xyz_masked"])
+    assert np.array_equal(O.build_uvxyz(x2d, xyz, 3, "quirk").numpy(), g["uvxyz_h3"])

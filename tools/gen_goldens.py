@@ -30,7 +30,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
+    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g7); default all")
     args = ap.parse_args()
+    only = set(x for x in args.only.split(",") if x)
+
+    def want(g):
+        return not only or g in only
     sys.path.insert(0, args.ref)
     sys.dont_write_bytecode = True
 
@@ -60,96 +65,162 @@ def main():
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model.eval()
     mask = torch.tensor([[[True] * 17]])
-    meta = {"weights_sha256": sha, "torch": torch.__version__, "generator": "tools/gen_goldens.py",
-            "reference": "nwicakson/diffpose-nw @ /root/reference"}
+    meta_path = os.path.join(args.out, "meta.json")
+    meta = json.load(open(meta_path)) if (only and os.path.exists(meta_path)) else {}
+    meta.update({"weights_sha256": sha, "torch": torch.__version__, "generator": "tools/gen_goldens.py",
+                 "reference": "nwicakson/diffpose-nw @ /root/reference"})
 
     # ---------------- G1: graph constants ----------------
-    L = ChebConv.get_laplacian(adj, True)
-    cheb = ChebConv(96, 96, K=2).cheb_polynomial(L)
-    lam = LAM_Gconv(96, 96)
-    lg = np.stack([lam.laplacian_batch(model.atten_layers[i].feed_forward.A_hat.detach()[None])[0].numpy()
-                   for i in range(5)])
-    np.savez(os.path.join(args.out, "g1_graph.npz"), adj=adj.numpy(), cheb=cheb.numpy(), lg=lg)
+    if want("g1"):
+        L = ChebConv.get_laplacian(adj, True)
+        cheb = ChebConv(96, 96, K=2).cheb_polynomial(L)
+        lam = LAM_Gconv(96, 96)
+        lg = np.stack([lam.laplacian_batch(model.atten_layers[i].feed_forward.A_hat.detach()[None])[0].numpy()
+                       for i in range(5)])
+        np.savez(os.path.join(args.out, "g1_graph.npz"), adj=adj.numpy(), cheb=cheb.numpy(), lg=lg)
 
     # ---------------- G2: per-module outputs ----------------
-    x6, _ = synthetic_batch(6, seed=101)
-    x6 = torch.from_numpy(x6)
-    with torch.no_grad():
-        t6 = torch.tensor([49.0, 0.0, 12.0, 12.0, 49.0, 31.0])
-        temb = get_timestep_embedding(t6, 96)
-        d0 = model.temb.dense[0](temb)
-        temb_full = model.temb.dense[1](nonlinearity(d0))
-        h_in = model.gconv_input(x6, adj)
-        al = model.atten_layers[0]
-        ln0 = al.sublayer[0].norm(h_in)
-        mha = al.self_attn(ln0, ln0, ln0, mask)
-        p_attn = al.self_attn.attn
-        x_a = h_in + mha
-        ln1 = al.sublayer[1].norm(x_a)
-        gn = al.feed_forward(ln1)
-        x_b = x_a + gn
-        res = model.gconv_layers[0](x_b, temb_full)
-        h_out_in = torch.randn(6, 17, 96, generator=torch.Generator().manual_seed(7))
-        cheb_out = model.gconv_output(h_out_in, adj)
-        eps = model(x6, mask, t6, 0)
-        # masked attention (a key mask with two False entries) through the whole model
-        mask2 = mask.clone()
-        mask2[0, 0, 3] = False
-        mask2[0, 0, 11] = False
-        eps_masked = model(x6, mask2, t6, 0)
-    np.savez(os.path.join(args.out, "g2_modules.npz"), x=x6.numpy(), t=t6.numpy(), temb=temb.numpy(),
-             temb_full=temb_full.numpy(), h_in=h_in.numpy(), ln0=ln0.numpy(), mha=mha.numpy(),
-             p_attn=p_attn.numpy(), x_a=x_a.numpy(), ln1=ln1.numpy(), graphnet=gn.numpy(),
-             x_b=x_b.numpy(), res_cheb=res.numpy(), h_out_in=h_out_in.numpy(), cheb_out=cheb_out.numpy(),
-             eps=eps.numpy(), mask2=mask2.numpy(), eps_masked=eps_masked.numpy())
+    if want("g2"):
+        x6, _ = synthetic_batch(6, seed=101)
+        x6 = torch.from_numpy(x6)
+        with torch.no_grad():
+            t6 = torch.tensor([49.0, 0.0, 12.0, 12.0, 49.0, 31.0])
+            temb = get_timestep_embedding(t6, 96)
+            d0 = model.temb.dense[0](temb)
+            temb_full = model.temb.dense[1](nonlinearity(d0))
+            h_in = model.gconv_input(x6, adj)
+            al = model.atten_layers[0]
+            ln0 = al.sublayer[0].norm(h_in)
+            mha = al.self_attn(ln0, ln0, ln0, mask)
+            p_attn = al.self_attn.attn
+            x_a = h_in + mha
+            ln1 = al.sublayer[1].norm(x_a)
+            gn = al.feed_forward(ln1)
+            x_b = x_a + gn
+            res = model.gconv_layers[0](x_b, temb_full)
+            h_out_in = torch.randn(6, 17, 96, generator=torch.Generator().manual_seed(7))
+            cheb_out = model.gconv_output(h_out_in, adj)
+            eps = model(x6, mask, t6, 0)
+            # masked attention (a key mask with two False entries) through the whole model
+            mask2 = mask.clone()
+            mask2[0, 0, 3] = False
+            mask2[0, 0, 11] = False
+            eps_masked = model(x6, mask2, t6, 0)
+        np.savez(os.path.join(args.out, "g2_modules.npz"), x=x6.numpy(), t=t6.numpy(), temb=temb.numpy(),
+                 temb_full=temb_full.numpy(), h_in=h_in.numpy(), ln0=ln0.numpy(), mha=mha.numpy(),
+                 p_attn=p_attn.numpy(), x_a=x_a.numpy(), ln1=ln1.numpy(), graphnet=gn.numpy(),
+                 x_b=x_b.numpy(), res_cheb=res.numpy(), h_out_in=h_out_in.numpy(), cheb_out=cheb_out.numpy(),
+                 eps=eps.numpy(), mask2=mask2.numpy(), eps_masked=eps_masked.numpy())
 
     # ---------------- G3/G4: sampler trajectories ----------------
-    def betas_for(T):
-        b = get_beta_schedule("linear", beta_start=0.0001, beta_end=0.001, num_diffusion_timesteps=T)
-        return torch.from_numpy(b).float()
+    if want("g34"):
+        def betas_for(T):
+            b = get_beta_schedule("linear", beta_start=0.0001, beta_end=0.001, num_diffusion_timesteps=T)
+            return torch.from_numpy(b).float()
 
-    def run(n, seq, T, seed, eta=0.0):
-        x, tgt = synthetic_batch(n, seed=seed)
-        x = torch.from_numpy(x)
-        xs, x0s = generalized_steps(x, mask, seq, model, betas_for(T), eta=eta)
-        return x.numpy(), tgt, xs, x0s
+        def run(n, seq, T, seed, eta=0.0):
+            x, tgt = synthetic_batch(n, seed=seed)
+            x = torch.from_numpy(x)
+            xs, x0s = generalized_steps(x, mask, seq, model, betas_for(T), eta=eta)
+            return x.numpy(), tgt, xs, x0s
 
-    seq10 = list(range(0, 50, 5))
-    x, tgt, xs, x0s = run(64, seq10, 51, 202)
-    out = xs[-1]
-    xyz = out[:, :, 2:].clone()
-    xyz = xyz - xyz[:, :1, :].clone()
-    tt = torch.from_numpy(tgt)
-    np.savez(os.path.join(args.out, "g3_traj_n64_k10.npz"), x=x, seq=np.array(seq10), T=51,
-             xs=torch.stack(xs).numpy(), x0s=torch.stack(x0s).numpy(), targets=tgt,
-             mpjpe_mm=np.float64(mpjpe(xyz, tt).item() * 1000.0))
+        seq10 = list(range(0, 50, 5))
+        x, tgt, xs, x0s = run(64, seq10, 51, 202)
+        out = xs[-1]
+        xyz = out[:, :, 2:].clone()
+        xyz = xyz - xyz[:, :1, :].clone()
+        tt = torch.from_numpy(tgt)
+        np.savez(os.path.join(args.out, "g3_traj_n64_k10.npz"), x=x, seq=np.array(seq10), T=51,
+                 xs=torch.stack(xs).numpy(), x0s=torch.stack(x0s).numpy(), targets=tgt,
+                 mpjpe_mm=np.float64(mpjpe(xyz, tt).item() * 1000.0))
 
-    seq50 = list(range(0, 50, 1))
-    x, tgt, xs, x0s = run(16, seq50, 51, 303)
-    np.savez(os.path.join(args.out, "g4_final_n16_k50.npz"), x=x, seq=np.array(seq50), T=51,
-             out=xs[-1].numpy(), x0_last=x0s[-1].numpy(), targets=tgt)
+        seq50 = list(range(0, 50, 1))
+        x, tgt, xs, x0s = run(16, seq50, 51, 303)
+        np.savez(os.path.join(args.out, "g4_final_n16_k50.npz"), x=x, seq=np.array(seq50), T=51,
+                 out=xs[-1].numpy(), x0_last=x0s[-1].numpy(), targets=tgt)
 
-    seq100 = list(range(0, 100, 1))
-    x, tgt, xs, x0s = run(16, seq100, 101, 404)
-    np.savez(os.path.join(args.out, "g4_final_n16_k100_T101.npz"), x=x, seq=np.array(seq100), T=101,
-             out=xs[-1].numpy(), x0_last=x0s[-1].numpy(), targets=tgt)
+        seq100 = list(range(0, 100, 1))
+        x, tgt, xs, x0s = run(16, seq100, 101, 404)
+        np.savez(os.path.join(args.out, "g4_final_n16_k100_T101.npz"), x=x, seq=np.array(seq100), T=101,
+                 out=xs[-1].numpy(), x0_last=x0s[-1].numpy(), targets=tgt)
 
-    seqq = [int(s) for s in list(np.linspace(0, np.sqrt(50 * 0.8), 10) ** 2)]   # quad skip, has duplicates
-    x, tgt, xs, x0s = run(8, seqq, 51, 505)
-    np.savez(os.path.join(args.out, "g4_final_n8_quad.npz"), x=x, seq=np.array(seqq), T=51,
-             out=xs[-1].numpy(), targets=tgt)
+        seqq = [int(s) for s in list(np.linspace(0, np.sqrt(50 * 0.8), 10) ** 2)]   # quad skip, has duplicates
+        x, tgt, xs, x0s = run(8, seqq, 51, 505)
+        np.savez(os.path.join(args.out, "g4_final_n8_quad.npz"), x=x, seq=np.array(seqq), T=51,
+                 out=xs[-1].numpy(), targets=tgt)
 
     # ---------------- G5: in-place root subtraction quirk ----------------
-    q = torch.from_numpy(synthetic_batch(3, seed=606)[0][:, :, 2:].copy())
-    q_in = q.clone()
-    q[:, :, :] -= q[:, :1, :]
-    try:
-        q1 = q_in[:1].clone()
-        q1[:, :, :] -= q1[:, :1, :]
-        b1_raises = False
-    except RuntimeError:
-        b1_raises = True
-    np.savez(os.path.join(args.out, "g5_root_quirk.npz"), x=q_in.numpy(), out=q.numpy(), b1_raises=b1_raises)
+    if want("g5"):
+        q = torch.from_numpy(synthetic_batch(3, seed=606)[0][:, :, 2:].copy())
+        q_in = q.clone()
+        q[:, :, :] -= q[:, :1, :]
+        try:
+            q1 = q_in[:1].clone()
+            q1[:, :, :] -= q1[:, :1, :]
+            b1_raises = False
+        except RuntimeError:
+            b1_raises = True
+        np.savez(os.path.join(args.out, "g5_root_quirk.npz"), x=q_in.numpy(), out=q.numpy(), b1_raises=b1_raises)
+
+    # ---------------- G6: GCNpose front-end + uvxyz assembly ----------------
+    if want("g6"):
+        from models.gcnpose import GCNpose
+
+        psd = synthetic_state_dict(kind="pose")
+        pcfg = types.SimpleNamespace(model=types.SimpleNamespace(
+            hid_dim=96, emd_dim=96, coords_dim=[2, 3], num_layer=5, n_head=4, dropout=0.25, n_pts=17))
+        pm = GCNpose(adj, pcfg)
+        pm.load_state_dict({k: torch.from_numpy(v) for k, v in psd.items()})
+        pm.eval()
+        x12, _ = synthetic_batch(12, seed=707)
+        x2d = torch.from_numpy(np.ascontiguousarray(x12[:, :, :2]))
+        mask2 = mask.clone()
+        mask2[0, 0, 5] = False
+        with torch.no_grad():
+            xyz = pm(x2d, mask)
+            xyz_masked = pm(x2d, mask2)
+            # test_hyber's assembly (runners/diffpose_frame.py:337-342), same torch ops
+            inputs_xyz = xyz.clone()
+            inputs_xyz[:, :, :] -= inputs_xyz[:, :1, :]
+            uvxyz = torch.cat([x2d, inputs_xyz], dim=2).repeat(3, 1, 1)
+        np.savez(os.path.join(args.out, "g6_gcnpose.npz"), x2d=x2d.numpy(), xyz=xyz.numpy(),
+                 xyz_masked=xyz_masked.numpy(), mask2=mask2.numpy(), uvxyz_h3=uvxyz.numpy())
+        meta["pose_weights_sha256"] = state_dict_sha256(psd, kind="pose")
+
+    # ---------------- G7: metrics and per-action accounting ----------------
+    if want("g7"):
+        from common.loss import mpjpe as loss_mpjpe, p_mpjpe as loss_p_mpjpe
+        from common.utils import define_error_list, print_error, test_calculation
+        from common.utils import p_mpjpe as utils_p_mpjpe
+
+        rng = np.random.Generator(np.random.PCG64(808))
+        n = 48
+        tgt = rng.normal(0.0, 0.25, size=(n, 17, 3))
+        tgt = tgt - tgt[:, :1]
+        pred = np.empty_like(tgt)
+        for i in range(n):                      # scaled, rotated (some reflected), shifted, noisy
+            q, _ = np.linalg.qr(rng.normal(size=(3, 3)))
+            if i % 5 == 0:
+                q[:, 0] = -q[:, 0] if np.linalg.det(q) > 0 else q[:, 0]
+            pred[i] = rng.uniform(0.7, 1.3) * tgt[i] @ q + rng.normal(0, 0.1, 3) + rng.normal(0, 0.03, (17, 3))
+        tgt = tgt.astype(np.float32)
+        pred = pred.astype(np.float32)
+        names = ["Directions", "Discussion", "Eating", "Greeting", "Phoning", "Photo", "Posing", "Purchases",
+                 "Sitting", "SittingDown", "Smoking", "Waiting", "WalkDog", "Walking", "WalkTogether"]
+        acts = ["Walking 1"] * 16 + [names[int(k)] + ("" if k % 3 == 0 else f" {1 + int(k) % 2}")
+                                     for k in rng.integers(0, 15, size=n - 16)]
+        bounds = [(0, 16), (16, 32), (32, 48)]
+        err = define_error_list(names)
+        for lo, hi in bounds:
+            test_calculation(torch.from_numpy(pred[lo:hi]), torch.from_numpy(tgt[lo:hi]), acts[lo:hi], err, None, None)
+        p1, p2 = print_error(None, err, 1)
+        np.savez(os.path.join(args.out, "g7_metrics.npz"), pred=pred, tgt=tgt, actions=np.array(acts),
+                 bounds=np.array(bounds), per_pose_p2=utils_p_mpjpe(pred, tgt),
+                 loss_p2=np.float64(loss_p_mpjpe(pred, tgt)),
+                 loss_p1=np.float64(loss_mpjpe(torch.from_numpy(pred), torch.from_numpy(tgt)).item()),
+                 p1=np.float64(p1), p2=np.float64(p2), action_names=np.array(names),
+                 action_p1=np.array([err[a]["p1"].avg for a in names], dtype=np.float64),
+                 action_p2=np.array([err[a]["p2"].avg for a in names], dtype=np.float64))
 
     with open(os.path.join(args.out, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
