@@ -30,6 +30,11 @@
 #define DPK_ABLATE 0
 #endif
 #define DPK_RUN(bit) ((DPK_ABLATE & (bit)) == 0)
+// Phase tracing builds (tools/phase_trace.py): lane 0 of every wave stamps s_memtime before and
+// after each workgroup barrier of one chosen DDIM step.
+#ifndef DPK_TRACE
+#define DPK_TRACE 0
+#endif
 #ifndef DPK_EXP
 #define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
 #endif
@@ -138,7 +143,12 @@ struct SampleArgs {
     unsigned mask;        // 17-bit key mask
     float eta;
     unsigned long long seed;
+#if DPK_TRACE
+    unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
+    int trace_step;
+#endif
 };
+constexpr int TRACE_SLOTS = 256;
 
 // ---------------------------------------------------------------------------------------
 // counter-based normal noise for eta > 0 (Philox4x32-10 + Box-Muller)
@@ -183,63 +193,95 @@ __device__ __forceinline__ int opaque(int x) {
 
 // ---------------------------------------------------------------------------------------
 // GEMM over the workgroup's 68 rows.  Rows 0..63 are 4 MFMA row tiles (v_mfma_f32_16x16x4_f32);
-// the 4 leftover rows 64..67 ("tail") are computed on the VALU inside the same k-loop from the
-// B fragments already in registers, so no MFMA work is spent on padding rows.
+// the 4 leftover rows 64..67 ("tail") are computed with scalar v_fma_f32 inside the same k-loop
+// from the B fragments already in registers: one FMA per MFMA, interleaved into the MFMA
+// stream (sched_group_barrier), where a single-issue VALU op hides in the MFMA's issue gap
+// (MI355X_MICROARCH.md: packed f32 ops beside MFMAs cost ~22 cycles each and 4x4x1_16b
+// MFMAs ~20 — both measured slower than this).
 //
 // MFMA operand maps: lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for sub-step j,
 // and the packed B block holds W[k = same][n = ct*16 + (l&15)] (a consistent permutation of k).
 // Tail: lane l accumulates, for tail row t and its column (l&15) of col tile c, the partial sum
 // over its own 4 k's of every k-block; the 4 lane groups are summed with two xor-shuffles.
 //
-// Wave w owns row tiles {2*(w>>1), 2*(w>>1)+1}, col tiles [(w&1)*NC/2, (w&1+1)*NC/2) and tail
-// rows 64 + 2*(w>>1) + {0,1} over the same columns: the four waves carry equal work.
-// The k-loop is a 2-stage register ring (named buffers, unrolled by 2): the B (global/L2) and
-// A (LDS) fragments of k-block kb+1 are in flight while the MFMAs of kb issue.
-template <int NR, int NCW, int TR, int KB0, int KB1>
-struct GemmTile {
-    static constexpr int KB = KB0 + KB1;
-    static constexpr int TA = TR > 0 ? TR : 1;
-    f32x4 acc[NR][NCW];
-    f32x2 tl[NCW][TA];      // tail partial sums: (.x, .y) = even / odd k of this lane's k's
-    int aoff0[NR], aoff1[NR], toff0[TA], toff1[TA];
+// B blocks are fetched with buffer loads: one VGPR offset (lane*16) shared by every load and the
+// block offset in SGPR soffset, so the k-loop does no VALU address arithmetic.  A comes from one
+// LDS buffer per GEMM (the Chebyshev GEMMs read [T1X | T2X | X] from B2, see cheb_prep), which
+// keeps the loop body a single basic block: loads are unconditional (last pair peeled) and the
+// compiler emits exact vmcnt/lgkmcnt waits instead of draining at a join.
+struct BSrc {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int voff;      // lane * 16
+    int sbase;     // byte offset of this wave's first column tile (wave-uniform)
+    __device__ __forceinline__ f32x4 load(int blk) const {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, sbase + blk * 1024, 0));
+    }
+};
 
-    __device__ __forceinline__ void loadA(f32x4 (&a)[NR], f32x4 (&t)[TA], const float* A0, const float* A1,
-                                          int kb) const {
-        if (kb < KB0) {
+// Packed B-fragment blocks of a GEMM with NC column tiles and KB k-blocks: [NC][KB][64 lanes][4].
+template <int NC, int KB>
+__device__ __forceinline__ BSrc bsrc(const float* Bp, int ct0, int lane) {
+    BSrc s;
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, NC * KB * 1024, 0x00020000);
+    s.voff = lane * 16;
+    s.sbase = ct0 * KB * 1024;
+    return s;
+}
+
+// Tail modes: TM_VALU — TR tail rows per wave on the VALU (scalar fma per MFMA);
+// TM_MFMA4 — all 4 tail rows on v_mfma_f32_4x4x1_16b_f32 for NQ = ceil(NCW/2) of the wave's
+// column tiles.  The 4x4x1 form reads the SAME B fragment as the 16x16x4 MFMAs (block b = l>>2
+// holds W[k = kb*16 + 4*(l>>4) + j][col 4*(b&3) + (l&3)]), and its A operand is one float per
+// lane: tail row l&3 at the lane group's k.  D reg r of lane l = partial sum (tail row r,
+// column l&15, k-slice l>>4).  The two waves of a column half split the tail column tiles: the
+// second wave processes its tiles rotated by NQ (rotation lives in SGPR load offsets and store
+// addresses only), so the tail tiles are local indices 0..NQ-1 for both.
+enum { TM_NONE = 0, TM_VALU = 1, TM_MFMA4 = 2 };
+
+template <int NR, int NCW, int TM, int TR, int KB>
+struct GemmTile {
+    static constexpr int TA = TM == TM_VALU ? TR : 1;    // tail A fragments per ring slot
+    static constexpr int NQ = TM == TM_MFMA4 ? (NCW + 1) / 2 : 1;
+    f32x4 acc[NR][NCW];
+    float tl[NCW][TA];      // TM_VALU: tail partial sums over this lane's k's
+    f32x4 tacc[NQ];         // TM_MFMA4: 4x4x1 accumulators
+    int aoff[NR], toff[TA];
+
+    __device__ __forceinline__ void loadA(f32x4 (&a)[NR], f32x4 (&t)[TA], const float* A, int kb) const {
 #pragma unroll
-            for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A0 + aoff0[i] + kb * 16);
+        for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A + aoff[i] + kb * 16);
+        if constexpr (TM != TM_NONE) {
 #pragma unroll
-            for (int i = 0; i < TR; ++i) t[i] = *reinterpret_cast<const f32x4*>(A0 + toff0[i] + kb * 16);
-        } else {
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(A1 + aoff1[i] + (kb - KB0) * 16);
-#pragma unroll
-            for (int i = 0; i < TR; ++i)
-                t[i] = *reinterpret_cast<const f32x4*>(A1 + toff1[i] + (kb - KB0) * 16);
+            for (int i = 0; i < TA; ++i) t[i] = *reinterpret_cast<const f32x4*>(A + toff[i] + kb * 16);
         }
     }
-    __device__ __forceinline__ static void loadB(f32x4 (&b)[NCW], const f32x4* __restrict__ Bl, int kb) {
+    __device__ __forceinline__ static void loadB(f32x4 (&b)[NCW], const BSrc& s, const int (&soff)[NCW], int kb) {
 #pragma unroll
-        for (int c = 0; c < NCW; ++c) b[c] = Bl[(c * KB + kb) * 64];
+        for (int c = 0; c < NCW; ++c)
+            b[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c] + kb * 1024, 0));
     }
     __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&t)[TA], const f32x4 (&b)[NCW]) {
 #pragma unroll
-        for (int jp = 0; jp < 4; jp += 2) {
+        for (int j = 0; j < 4; ++j) {
 #pragma unroll
-            for (int j = jp; j < jp + 2; ++j)
+            for (int i = 0; i < NR; ++i)
 #pragma unroll
-                for (int i = 0; i < NR; ++i)
+                for (int c = 0; c < NCW; ++c)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+            if constexpr (TM == TM_VALU) {
 #pragma unroll
-                    for (int c = 0; c < NCW; ++c)
-                        acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+                for (int c = 0; c < NCW; ++c)
 #pragma unroll
-            for (int c = 0; c < NCW; ++c)
+                    for (int r = 0; r < TR; ++r) tl[c][r] = fmaf(t[r][j], b[c][j], tl[c][r]);
+            } else if constexpr (TM == TM_MFMA4) {
 #pragma unroll
-                for (int r = 0; r < TR; ++r)
-                    tl[c][r] = pfma(f32x2{t[r][jp], t[r][jp + 1]}, f32x2{b[c][jp], b[c][jp + 1]}, tl[c][r]);
+                for (int q = 0; q < NQ; ++q) tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(t[0][j], b[q][j], tacc[q], 0, 0, 0);
+            }
         }
     }
+    // keep the ring's program order: this half's MFMAs, then its slot's loads; nothing crosses
+    // (otherwise the scheduler sinks the loads next to their consumers)
+    __device__ __forceinline__ static void schedule_half() { __builtin_amdgcn_sched_barrier(0); }
 };
 
 // B fragments of a GEMM's first two k-blocks, loaded before the phase that precedes the GEMM
@@ -249,17 +291,32 @@ struct BPre {
     f32x4 b0[NCW], b1[NCW];
 };
 
-// Column tiles per streamed pass (see gemm_stream).
-constexpr int CW = 3;
+// Column rotation of wave `wave` within its column half (TM_MFMA4 tail split, see GemmTile).
+template <int NCW>
+__device__ __forceinline__ int col_rot(int wave) { return (wave >> 1) ? (NCW + 1) / 2 : 0; }
+
+// SGPR byte offsets of the wave's NCW column tiles' first k-block, rotation applied.
+template <int NCW, int KB>
+__device__ __forceinline__ void tile_offsets(int (&soff)[NCW], int sbase, int rot) {
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+        const int cc = c + rot;
+        soff[c] = sbase + (cc >= NCW ? cc - NCW : cc) * KB * 1024;
+    }
+}
 
 template <int NC, int KB>
 __device__ __forceinline__ BPre<NC / 2> gemm_prefetch(const float* Bp, int wave, int lane) {
-    BPre<NC / 2> pre;
-    const f32x4* Bl = reinterpret_cast<const f32x4*>(Bp) + (size_t)((wave & 1) * (NC / 2)) * KB * 64 + lane;
+    constexpr int NCW = NC / 2;
+    const BSrc s = bsrc<NC, KB>(Bp, (wave & 1) * NCW, lane);
+    int soff[NCW];
+    tile_offsets<NCW, KB>(soff, s.sbase, col_rot<NCW>(wave));
+    BPre<NCW> pre;
 #pragma unroll
-    for (int c = 0; c < NC / 2; ++c) {
-        pre.b0[c] = Bl[(c * KB + 0) * 64];
-        pre.b1[c] = KB > 1 ? Bl[(c * KB + 1) * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < NCW; ++c) {
+        pre.b0[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c], 0));
+        pre.b1[c] = KB > 1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c] + 1024, 0))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     return pre;
 }
@@ -302,17 +359,17 @@ __device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, fl
     return e.tproj[(size_t)pose * e.tproj_pose_stride + col];
 }
 
-// One wave, single pass: row tiles [rt0, rt0+NR) on MFMA and tail rows trow0.. on VALU over
-// NCW column tiles from ct0; 2-stage register ring (named buffers, unrolled by 2).  Used for
-// the wide GEMMs (QKV: 9, fc1: 6 column tiles per wave).
-template <int NR, int NCW, int TR, int KB0, int KB1, int MODE>
-__device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float* A1, int lda1,
-                                          const f32x4* __restrict__ Bp, int rt0, int ct0, int trow0, int lane,
-                                          const EpiArgs& e, const BPre<NCW>& pre) {
-    using T = GemmTile<NR, NCW, TR, KB0, KB1>;
-    constexpr int KB = T::KB;
-    constexpr int TA = T::TA;
-    static_assert(KB % 2 == 0, "k-blocks in pairs");
+
+// One wave: row tiles [rt0, rt0+NR) on MFMA plus the tail (TM) over NCW column tiles from ct0,
+// visited in rotated order (local tile c = global ct0 + (c + rot) mod NCW); 2-stage register
+// ring (named buffers, loop unrolled by 2, last pair peeled).
+template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE>
+__device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* Bp, int rt0, int ct0, int rot,
+                                          int trow0, bool tail_dup, int lane, const EpiArgs& e,
+                                          const BPre<NCW>& pre) {
+    using T = GemmTile<NR, NCW, TM, TR, KB>;
+    constexpr int TA = T::TA, NQ = T::NQ;
+    static_assert(KB == 1 || KB % 2 == 0, "k-blocks in pairs");
     lane = opaque(lane);
     T g;
 #pragma unroll
@@ -322,49 +379,60 @@ __device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float
 #pragma unroll
     for (int c = 0; c < NCW; ++c)
 #pragma unroll
-        for (int r = 0; r < TA; ++r) g.tl[c][r] = f32x2{0.f, 0.f};
+        for (int r = 0; r < TA; ++r) g.tl[c][r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) g.tacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int rl = lane & 15, kq = (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int r = (rt0 + i) * 16 + rl;
-        g.aoff0[i] = r * lda0 + kq;
-        g.aoff1[i] = r * lda1 + kq;
-    }
+    for (int i = 0; i < NR; ++i) g.aoff[i] = ((rt0 + i) * 16 + rl) * lda + kq;
+    if constexpr (TM == TM_MFMA4) {
+        g.toff[0] = (trow0 + (lane & 3)) * lda + kq;
+    } else {
 #pragma unroll
-    for (int i = 0; i < TA; ++i) {
-        g.toff0[i] = (trow0 + i) * lda0 + kq;
-        g.toff1[i] = (trow0 + i) * lda1 + kq;
+        for (int i = 0; i < TA; ++i) g.toff[i] = (trow0 + i) * lda + kq;
+    }
+    int gcol[NCW];                                  // global column tile of local tile c (uniform)
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+        const int cc = c + rot;
+        gcol[c] = ct0 + (cc >= NCW ? cc - NCW : cc);
     }
     float bcol[NCW], tcol[NCW];
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
-        const int col = (ct0 + c) * 16 + rl;
+        const int col = gcol[c] * 16 + rl;
         bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[col];
         tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
     }
-    const f32x4* Bl = Bp + (size_t)ct0 * KB * 64 + lane;
+    const BSrc src = bsrc<NC, KB>(Bp, ct0, lane);
+    int soff[NCW];
+    tile_offsets<NCW, KB>(soff, src.sbase, rot);
     f32x4 a0[NR], t0[TA], b0[NCW], a1[NR], t1[TA], b1[NCW];
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
         b0[c] = pre.b0[c];
         b1[c] = pre.b1[c];
     }
-    g.loadA(a0, t0, A0, A1, 0);
-    g.loadA(a1, t1, A0, A1, 1);
-#pragma unroll 1
-    for (int kb = 0; kb < KB; kb += 2) {
+    g.loadA(a0, t0, A, 0);
+    if constexpr (KB == 1) {
         g.mma(a0, t0, b0);
-        if (kb + 2 < KB) {
-            T::loadB(b0, Bl, kb + 2);
-            g.loadA(a0, t0, A0, A1, kb + 2);
+    } else {
+        g.loadA(a1, t1, A, 1);
+#pragma unroll 1
+        for (int kb = 0; kb < KB - 2; kb += 2) {
+            g.mma(a0, t0, b0);
+            T::loadB(b0, src, soff, kb + 2);
+            g.loadA(a0, t0, A, kb + 2);
+            T::schedule_half();
+            g.mma(a1, t1, b1);
+            T::loadB(b1, src, soff, kb + 3);
+            g.loadA(a1, t1, A, kb + 3);
+            T::schedule_half();
         }
+        g.mma(a0, t0, b0);
         g.mma(a1, t1, b1);
-        if (kb + 3 < KB) {
-            T::loadB(b1, Bl, kb + 3);
-            g.loadA(a1, t1, A0, A1, kb + 3);
-        }
     }
-    float* d = e.dst + ((rt0 * 16 + kq) * e.ldd + ct0 * 16 + rl);
+    float* d = e.dst + ((rt0 * 16 + kq) * e.ldd + rl);
     float old[NR][NCW][4];
     if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
 #pragma unroll
@@ -372,7 +440,7 @@ __device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float
 #pragma unroll
             for (int c = 0; c < NCW; ++c)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + c * 16];
+                for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + gcol[c] * 16];
     }
 #pragma unroll
     for (int i = 0; i < NR; ++i)
@@ -381,246 +449,111 @@ __device__ __forceinline__ void gemm_wave(const float* A0, int lda0, const float
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = (rt0 + i) * 16 + kq + r;
-                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (ct0 + c) * 16 + rl, tcol[c]) : 0.f;
-                d[(i * 16 + r) * e.ldd + c * 16] = epi_value<MODE>(
+                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[c] * 16 + rl, tcol[c]) : 0.f;
+                d[(i * 16 + r) * e.ldd + gcol[c] * 16] = epi_value<MODE>(
                     g.acc[i][c][r], bcol[c], tp, (MODE == E_RESID || MODE == E_RESID_RELU) ? old[i][c][r] : 0.f);
             }
-    if constexpr (TR > 0) {
+    const int grp = lane >> 4;
+    if constexpr (TM == TM_VALU) {
         float tv[NCW][TR];
 #pragma unroll
         for (int c = 0; c < NCW; ++c)
 #pragma unroll
             for (int r = 0; r < TR; ++r) {
-                float v = g.tl[c][r].x + g.tl[c][r].y;
+                float v = g.tl[c][r];
                 v += __shfl_xor(v, 16, 64);
                 v += __shfl_xor(v, 32, 64);
                 tv[c][r] = v;
             }
-        const int grp = lane >> 4;
         if (grp < TR) {
             const int row = trow0 + grp;
-            float* dt = e.dst + row * e.ldd + ct0 * 16 + rl;
+            float* dt = e.dst + row * e.ldd + rl;
 #pragma unroll
             for (int c = 0; c < NCW; ++c) {
                 float v = tv[c][0];
 #pragma unroll
                 for (int r = 1; r < TR; ++r)
                     if (grp == r) v = tv[c][r];
-                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[c * 16] : 0.f;
-                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (ct0 + c) * 16 + rl, tcol[c]) : 0.f;
-                dt[c * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
+                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[gcol[c] * 16] : 0.f;
+                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[c] * 16 + rl, tcol[c]) : 0.f;
+                dt[gcol[c] * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
             }
         }
-    }
-}
-
-// One wave, streamed: row tile rt on MFMA and tail row trow on VALU, over NP passes of CW column
-// tiles starting at ct0.  B/A/tail operands flow through a 3-stage register ring (named
-// buffers, loop unrolled by 3): step i computes with slot i%3 while slots (i+1)%3 and (i+2)%3
-// are in flight; passes are chained so the next pass's first fragments load under the
-// current pass's last MFMAs and epilogue.
-template <int NR, int TR, int NP, int KB0, int KB1, int MODE>
-__device__ __forceinline__ void gemm_stream(const float* A0, int lda0, const float* A1, int lda1,
-                                            const f32x4* __restrict__ Bp, int rt, int ct0, int trow, int lane,
-                                            const EpiArgs& e, const BPre<CW>& pre) {
-    using T = GemmTile<NR, CW, TR, KB0, KB1>;
-    constexpr int KB = T::KB;
-    constexpr int NS = NP * KB;                  // steps
-    static_assert(KB == 1 || KB % 3 == 0, "pass boundary at ring position 2");
-    lane = opaque(lane);
-    T g;
-    const int rl = lane & 15, kq = (lane >> 4) * 4;
+    } else if constexpr (TM == TM_MFMA4) {
+        // reduce the 4 k-slices; lane group g then writes tail row trow0 + g
+        const int row = trow0 + grp;
+        float* dt = e.dst + row * e.ldd + rl;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int r = (rt + i) * 16 + rl;
-        g.aoff0[i] = r * lda0 + kq;
-        g.aoff1[i] = r * lda1 + kq;
-    }
+        for (int q = 0; q < NQ; ++q) {
+            f32x4 v = g.tacc[q];
 #pragma unroll
-    for (int i = 0; i < TR; ++i) {
-        g.toff0[i] = (trow + i) * lda0 + kq;
-        g.toff1[i] = (trow + i) * lda1 + kq;
-    }
-    auto zero = [&]() {
-#pragma unroll
-        for (int c = 0; c < CW; ++c) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) g.acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < TR; ++i) g.tl[c][i] = f32x2{0.f, 0.f};
-        }
-    };
-    zero();
-    const f32x4* Bl = Bp + (size_t)ct0 * KB * 64 + lane;
-    // B block of step i: pass i/KB, kb i%KB -> column tiles ct0 + CW*pass + c
-    auto loadB = [&](f32x4 (&b)[CW], int i) {
-        const int pass = i / KB, kb = i - pass * KB;
-#pragma unroll
-        for (int c = 0; c < CW; ++c) b[c] = Bl[((pass * CW + c) * KB + kb) * 64];
-    };
-    auto loadA = [&](f32x4 (&a)[NR], f32x4 (&t)[TR], int i) { g.loadA(a, t, A0, A1, i % KB); };
-
-    // epilogue of pass `pass` (rows: MFMA tile + tail row)
-    auto epilogue = [&](int pass) {
-        const int cb = ct0 + pass * CW;
-        float bcol[CW], tcol[CW];
-#pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            const int col = (cb + c) * 16 + rl;
-            bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[col];
-            tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
-        }
-        float* d = e.dst + ((rt * 16 + kq) * e.ldd + cb * 16 + rl);
-        float old[NR][CW][4];
-        if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-#pragma unroll
-                for (int c = 0; c < CW; ++c)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + c * 16];
-        }
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < CW; ++c)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = (rt + i) * 16 + kq + r;
-                    const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (cb + c) * 16 + rl, tcol[c]) : 0.f;
-                    d[(i * 16 + r) * e.ldd + c * 16] = epi_value<MODE>(
-                        g.acc[i][c][r], bcol[c], tp, (MODE == E_RESID || MODE == E_RESID_RELU) ? old[i][c][r] : 0.f);
-                }
-        // tail rows: reduce the 4 lane groups' k-partials; lane group t writes tail row t
-        float tv[CW][TR];
-#pragma unroll
-        for (int c = 0; c < CW; ++c)
-#pragma unroll
-            for (int i = 0; i < TR; ++i) {
-                float v = g.tl[c][i].x + g.tl[c][i].y;
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
-                tv[c][i] = v;
+            for (int r = 0; r < 4; ++r) {
+                v[r] += __shfl_xor(v[r], 16, 64);
+                v[r] += __shfl_xor(v[r], 32, 64);
             }
-        const int grp = lane >> 4;
-        if (grp < TR) {
-            const int row = trow + grp;
-            float* dt = e.dst + row * e.ldd + cb * 16 + rl;
-#pragma unroll
-            for (int c = 0; c < CW; ++c) {
-                float v = tv[c][0];
-#pragma unroll
-                for (int i = 1; i < TR; ++i)
-                    if (grp == i) v = tv[c][i];
-                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[c * 16] : 0.f;
-                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, (cb + c) * 16 + rl, tcol[c]) : 0.f;
-                dt[c * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
-            }
+            const float x = grp == 0 ? v[0] : grp == 1 ? v[1] : grp == 2 ? v[2] : v[3];
+            if (q == NQ - 1 && tail_dup) continue;   // duplicate tile (odd NCW, second wave)
+            const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[gcol[q] * 16] : 0.f;
+            const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[q] * 16 + rl, tcol[q]) : 0.f;
+            dt[gcol[q] * 16] = epi_value<MODE>(x, bcol[q], tp, old_t);
         }
-        zero();
-    };
-
-    f32x4 aS0[NR], tS0[TR], bS0[CW], aS1[NR], tS1[TR], bS1[CW], aS2[NR], tS2[TR], bS2[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) {
-        bS0[c] = pre.b0[c];
-        bS1[c] = pre.b1[c];
-    }
-    loadA(aS0, tS0, 0);
-    if constexpr (KB == 1) {                    // gconv_input: one k-block per pass
-        static_assert(NP == 1, "single pass");
-        g.mma(aS0, tS0, bS0);
-        epilogue(0);
-        return;
-    }
-    loadA(aS1, tS1, 1);
-#pragma unroll 1
-    for (int i = 0; i < NS; i += 3) {
-        if (i + 2 < NS) {
-            loadB(bS2, i + 2);
-            loadA(aS2, tS2, i + 2);
-        }
-        g.mma(aS0, tS0, bS0);
-        if (i + 3 < NS) {
-            loadB(bS0, i + 3);
-            loadA(aS0, tS0, i + 3);
-        }
-        g.mma(aS1, tS1, bS1);
-        if (i + 4 < NS) {
-            loadB(bS1, i + 4);
-            loadA(aS1, tS1, i + 4);
-        }
-        g.mma(aS2, tS2, bS2);
-        if ((i + 2) % KB == KB - 1) epilogue((i + 2) / KB);
     }
 }
 
 // Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
-// 2*(w>>1)+1, column half w&1, tail rows 64 + 2*(w>>1) + {0,1}: equal work per wave, 128 B of
-// B fragment per MFMA; 2-stage single-pass register ring (the 3-stage streamed variant measured
-// slower for every shape here and is kept for the single-k-block gconv_input only).
-template <int NC, int KB0, int KB1, int MODE>
-__device__ __forceinline__ void gemm_wg(const float* A0, int lda0, const float* A1, int lda1, const float* Bp,
-                                        int wave, int lane, const EpiArgs& e, const BPre<NC / 2>& pre) {
+// 2*(w>>1)+1 and column half w&1 on the 16x16x4 MFMA; the 4 tail rows 64..67 of that column
+// half on 4x4x1 MFMAs, split between the half's two waves (rotated column order for w>>1 = 1).
+template <int NC, int KB, int MODE>
+__device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp, int wave, int lane,
+                                        const EpiArgs& e, const BPre<NC / 2>& pre) {
     static_assert(NC % 2 == 0 && R == 68 && NW == 4, "4 row tiles x 2 column halves + 4 tail rows");
-    const f32x4* B = reinterpret_cast<const f32x4*>(Bp);
+    constexpr int NCW = NC / 2;
     const int half = wave >> 1;
-    if constexpr (KB0 + KB1 == 1)            // gconv_input: a single k-block
-        gemm_stream<2, 2, 1, KB0, KB1, MODE>(A0, lda0, A1, lda1, B, 2 * half, (wave & 1) * (NC / 2), 64 + 2 * half,
-                                             lane, e, pre);
-    else
-        gemm_wave<2, NC / 2, 2, KB0, KB1, MODE>(A0, lda0, A1, lda1, B, 2 * half, (wave & 1) * (NC / 2),
-                                                64 + 2 * half, lane, e, pre);
+    const bool dup = (NCW & 1) && half == 1;
+    gemm_wave<2, NCW, TM_MFMA4, 0, NC, KB, MODE>(A, lda, Bp, 2 * half, (wave & 1) * NCW, col_rot<NCW>(wave), 64, dup,
+                                                 lane, e, pre);
 }
 
 // Output ChebConv (96->5, one col tile): waves 0-3, wave w = row tile w + tail row 64+w; the
 // raw accumulators go to a functor (DDIM update).
 template <int KB>
 __device__ __forceinline__ BPre<1> out_prefetch(const float* Bp, int lane) {
+    const BSrc s = bsrc<1, KB>(Bp, 0, lane);
     BPre<1> pre;
-    const f32x4* Bl = reinterpret_cast<const f32x4*>(Bp) + lane;
-    pre.b0[0] = Bl[0];
-    pre.b1[0] = Bl[64];
+    pre.b0[0] = s.load(0);
+    pre.b1[0] = s.load(1);
     return pre;
 }
 
-template <int KB0, int KB1, class Epi>
-__device__ __forceinline__ void gemm_out(const float* A0, int lda0, const float* A1, int lda1,
-                                         const f32x4* __restrict__ Bp, int wave, int lane, Epi epi,
+template <int KB, class Epi>
+__device__ __forceinline__ void gemm_out(const float* A, int lda, const float* Bp, int wave, int lane, Epi epi,
                                          const BPre<1>& pre) {
-    using T = GemmTile<1, 1, 1, KB0, KB1>;
-    constexpr int KB = T::KB;
+    using T = GemmTile<1, 1, TM_VALU, 1, KB>;
+    static_assert(KB % 2 == 0, "k-blocks in pairs");
     lane = opaque(lane);
     T g;
     g.acc[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g.tl[0][0] = f32x2{0.f, 0.f};
+    g.tl[0][0] = 0.f;
     const int rl = lane & 15, kq = (lane >> 4) * 4;
-    {
-        const int r = wave * 16 + rl;
-        g.aoff0[0] = r * lda0 + kq;
-        g.aoff1[0] = r * lda1 + kq;
-        const int tr = 64 + wave;
-        g.toff0[0] = tr * lda0 + kq;
-        g.toff1[0] = tr * lda1 + kq;
-    }
-    const f32x4* Bl = Bp + lane;
+    g.aoff[0] = (wave * 16 + rl) * lda + kq;
+    g.toff[0] = (64 + wave) * lda + kq;
+    const BSrc src = bsrc<1, KB>(Bp, 0, lane);
+    const int soff[1] = {0};
     f32x4 a0[1], t0[1], b0[1] = {pre.b0[0]}, a1[1], t1[1], b1[1] = {pre.b1[0]};
-    g.loadA(a0, t0, A0, A1, 0);
-    g.loadA(a1, t1, A0, A1, 1);
+    g.loadA(a0, t0, A, 0);
+    g.loadA(a1, t1, A, 1);
 #pragma unroll 1
-    for (int kb = 0; kb < KB; kb += 2) {
+    for (int kb = 0; kb < KB - 2; kb += 2) {
         g.mma(a0, t0, b0);
-        if (kb + 2 < KB) {
-            T::loadB(b0, Bl, kb + 2);
-            g.loadA(a0, t0, A0, A1, kb + 2);
-        }
+        T::loadB(b0, src, soff, kb + 2);
+        g.loadA(a0, t0, A, kb + 2);
         g.mma(a1, t1, b1);
-        if (kb + 3 < KB) {
-            T::loadB(b1, Bl, kb + 3);
-            g.loadA(a1, t1, A0, A1, kb + 3);
-        }
+        T::loadB(b1, src, soff, kb + 3);
+        g.loadA(a1, t1, A, kb + 3);
     }
-    float tv = g.tl[0][0].x + g.tl[0][0].y;
+    g.mma(a0, t0, b0);
+    g.mma(a1, t1, b1);
+    float tv = g.tl[0][0];
     tv += __shfl_xor(tv, 16, 64);
     tv += __shfl_xor(tv, 32, 64);
     if (rl < COUT) {
@@ -629,7 +562,6 @@ __device__ __forceinline__ void gemm_out(const float* A0, int lda0, const float*
         if (kq == 0) epi(64 + wave, rl, tv);
     }
 }
-
 // ---------------------------------------------------------------------------------------
 // Correctly rounded x / d from a shared reciprocal r = 1/d (Markstein: one fma residual
 // correction).  Used where a whole row is divided by one value (LayerNorm).
@@ -838,7 +770,8 @@ constexpr SparsePattern make_pattern() {
 constexpr SparsePattern SPAT = make_pattern();
 static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 
-// Chebyshev prologue: B2[:, 0:96] = T1 src, B2[:, 96:192] = T2 src (ChebConv.py:83).
+// Chebyshev prologue: B2 = [T1 src | T2 src | src] (ChebConv.py:83, term order rotated so the
+// K=288 GEMM reads one buffer; the packed weights follow the same order).
 // One thread per (pose, column pair).  SPARSE: compile-time pattern, packed values (scalar
 // loads); dense: 17x17 from the arena.  Sums run over increasing i in both (identical bits).
 template <bool SPARSE>
@@ -870,6 +803,7 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
         }
         *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
         *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
+        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = v[j];
     }
 }
 
@@ -941,7 +875,11 @@ __device__ __forceinline__ void input_prep(const float* __restrict__ cw, const f
 // The sampler: K DDIM steps (or one eps evaluation, or one GCNpose forward) for P poses
 // per workgroup.
 template <int MODE, bool SPARSE>
-__global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
+// `arena` is a separate restrict kernel argument: the compiler can then prove the weight arena
+// is never written during the launch and turns its wave-uniform loads (Laplacians, Chebyshev
+// terms, LayerNorm gains, biases) into scalar s_load (in the SampleArgs struct it cannot, and
+// every such value became a vector load with its L2 latency exposed).
+__global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float* __restrict__ arena) {
     constexpr bool EPS_MODE = MODE == M_EPS;
     constexpr bool POSE = MODE == M_POSE;
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
@@ -955,7 +893,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
     const int pose0 = blockIdx.x * P;
     const int npose = min(P, a.N - pose0);
     const int nvalid = npose * PE;
-    const float* W = a.arena;
+    const float* W = arena;
     const float* CW = W + (SPARSE ? OFF_CHEBS : OFF_CHEB);
 
     if constexpr (POSE) {
@@ -970,17 +908,35 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
     __syncthreads();
 
     const int K = MODE == M_SAMPLE ? a.K : 1;
+#if DPK_TRACE
+    int tix = 0;
+    unsigned long long* trow = a.trace ? a.trace + ((size_t)blockIdx.x * NW + wave) * TRACE_SLOTS : nullptr;
+#define DPK_STAMP()                                                                        \
+    do {                                                                                   \
+        if (trow && s == a.trace_step && (tid & 63) == 0 && tix < TRACE_SLOTS)             \
+            trow[tix] = __builtin_amdgcn_s_memtime();                                      \
+        tix += (trow && s == a.trace_step) ? 1 : 0;                                        \
+    } while (0)
+#define BAR()          \
+    do {               \
+        DPK_STAMP();   \
+        __syncthreads(); \
+        DPK_STAMP();   \
+    } while (0)
+#else
+#define BAR() __syncthreads()
+#endif
 #pragma unroll 1
     for (int s = 0; s < K; ++s) {
         // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
         {
             const auto pre = gemm_prefetch<6, 1>(W + OFF_WIN, wave, lane);
             input_prep<SPARSE>(CW, XST, B1, tid);
-            __syncthreads();
+            BAR();
             const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1};
-            gemm_wg<6, 1, 0, E_STORE>(B1, LDX, nullptr, 0, W + OFF_WIN, wave, lane, e, pre);
+            gemm_wg<6, 1, E_STORE>(B1, LDX, W + OFF_WIN, wave, lane, e, pre);
         }
-        __syncthreads();
+        BAR();
 
 #pragma unroll 1
         for (int l = 0; l < NL; ++l) {
@@ -989,77 +945,76 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
             {
                 const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 32)) {
                     const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<18, 6, 0, E_STORE>(B1, LDX, nullptr, 0, LW + OFF_QKV, wave, lane, e, pre);
+                    gemm_wg<18, 6, E_STORE>(B1, LDX, LW + OFF_QKV, wave, lane, e, pre);
                 }
             }
-            __syncthreads();
+            BAR();
             {
                 const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
                 if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 64)) {
                     const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 6, 0, E_RESID>(B1, LDX, nullptr, 0, LW + OFF_O, wave, lane, e, pre);
+                    gemm_wg<6, 6, E_RESID>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
                 }
             }
-            __syncthreads();
+            BAR();
             // ---- x = x + GraphNet(LN1(x)) = x + L (relu((L LN1(x)) W1^T + b1) W2^T) + b2
             //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
             {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 128)) {
                     const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<12, 6, 0, E_STORE_RELU>(B1, LDX, nullptr, 0, LW + OFF_FC1, wave, lane, e, pre);
+                    gemm_wg<12, 6, E_STORE_RELU>(B1, LDX, LW + OFF_FC1, wave, lane, e, pre);
                 }
             }
             {
                 const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 256)) {
                     const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 12, 0, E_STORE_NB>(B2, LD2, nullptr, 0, LW + OFF_FC2, wave, lane, e, pre);
+                    gemm_wg<6, 12, E_STORE_NB>(B2, LD2, LW + OFF_FC2, wave, lane, e, pre);
                 }
             }
             {
                 const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
-                __syncthreads();
+                BAR();
                 // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
                 if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 512)) {
                     const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
                     const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
-                    gemm_wg<6, 6, 12, E_CHEB1>(XS, LDX, B2, LD2, LW + OFF_C1, wave, lane, e, pre);
+                    gemm_wg<6, 18, E_CHEB1>(B2, LD2, LW + OFF_C1, wave, lane, e, pre);
                 }
             }
             {
                 const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
-                __syncthreads();
+                BAR();
                 if (DPK_RUN(16 | 1024)) {
                     const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 6, 12, E_RESID_RELU>(B1, LDX, B2, LD2, LW + OFF_C2, wave, lane, e, pre);
+                    gemm_wg<6, 18, E_RESID_RELU>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
                 }
             }
-            __syncthreads();
+            BAR();
         }
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
         //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly)
         const auto preo = out_prefetch<18>(W + OFF_WOUT, lane);
         cheb_prep<SPARSE>(CW, XS, B2, tid);
-        __syncthreads();
+        BAR();
         {
-            const f32x4* Bo = reinterpret_cast<const f32x4*>(W + OFF_WOUT);
             float cf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
             if constexpr (MODE == M_SAMPLE) {
                 const float* cfp = a.coef + s * 6;
@@ -1087,9 +1042,9 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
                     }
                 }
             };
-            gemm_out<6, 12>(XS, LDX, B2, LD2, Bo, wave, lane, epi, preo);
+            gemm_out<18>(B2, LD2, W + OFF_WOUT, wave, lane, epi, preo);
         }
-        __syncthreads();
+        BAR();
     }
     if constexpr (MODE == M_SAMPLE) {
         for (int i = tid; i < nvalid; i += NT) a.x_out[(size_t)pose0 * PE + i] = XST[i];
@@ -1119,6 +1074,9 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a) {
             }
     }
 }
+
+#undef BAR
+#undef DPK_STAMP
 
 // ---------------------------------------------------------------------------------------
 // Timestep MLP (gcndiff.py:15-33, :103-106) and per-layer temb_proj(swish(.)) (:46, :51):
@@ -1203,6 +1161,11 @@ struct dpk_handle {
     bool profiling = false;
     bool sparse_graph = false;     // adjacency matches the compiled H36M Chebyshev pattern
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
+#if DPK_TRACE
+    unsigned long long* trace = nullptr;
+    size_t trace_len = 0;
+    int trace_step = -1;
+#endif
 };
 
 // event pair around a sampler-kernel launch (dpk_profile)
@@ -1246,6 +1209,10 @@ static void pack_blocks(float* dst, int Kreal, int Nreal, int KB, int NC, F w) {
                     dst[((size_t)(ct * KB + kb) * 64 + lane) * 4 + j] = (k < Kreal && n < Nreal) ? w(k, n) : 0.f;
                 }
 }
+
+// Row of a ChebConv weight (3,1,96,out) viewed as [3*96][out] that multiplies column k of
+// cheb_prep's [T1X | T2X | X] buffer.
+static inline int cheb_row(int k) { return ((k / D + 1) % 3) * D + k % D; }
 
 // Chebyshev terms of the normalised Laplacian, fp32 in the reference's operation order
 // (ChebConv.py:114-130, :90-112): d = rowsum^-1/2; L = I - (d_i g_ij) d_j; T2 = 2 L@L - I.
@@ -1455,9 +1422,9 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         pack_blocks(Lw + OFF_O, D, D, KB_D, 6, [&](int k, int n) { return wo[n * D + k]; });
         pack_blocks(Lw + OFF_FC1, D, D2, KB_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
         pack_blocks(Lw + OFF_FC2, D2, D, KB_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
-        // ChebConv weight (3,1,in,out): row k = order*in + c of the stacked [X|T1X|T2X]
-        pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[(k / D) * D * D + (k % D) * D + n]; });
-        pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[(k / D) * D * D + (k % D) * D + n]; });
+        // ChebConv weight (3,1,in,out), rows in cheb_prep's B2 order [T1X | T2X | X]: k -> order (k/96+1)%3
+        pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
+        pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
         for (int c = 0; c < D; ++c) {
             Lw[OFF_BQKV + c] = bq[c];
             Lw[OFF_BQKV + D + c] = bk[c];
@@ -1491,8 +1458,7 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         const int o = k / CIN, c = k % CIN;
         return c < cin ? wi[o * cin * D + c * D + n] : 0.f;
     });
-    pack_blocks(A + OFF_WOUT, D3, cout, KB_D3, 1,
-                [&](int k, int n) { return wout[(k / D) * D * cout + (k % D) * cout + n]; });
+    pack_blocks(A + OFF_WOUT, D3, cout, KB_D3, 1, [&](int k, int n) { return wout[cheb_row(k) * cout + n]; });
     for (int c = 0; c < D; ++c) A[OFF_BIN + c] = bi[c];
     for (int c = 0; c < 16; ++c) A[OFF_BOUT + c] = c < cout ? bout[c] : 0.f;
     if (!pose) {         // GCNpose carries temb.dense too (gcnpose.py:94-98) but never uses it
@@ -1597,9 +1563,9 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_EPS, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_EPS, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     else
-        hipLaunchKernelGGL((sample_kernel<M_EPS, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_EPS, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -1633,12 +1599,25 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.mask = h->mask;
     a.eta = h->eta;
     a.seed = seed;
+#if DPK_TRACE
+    if (h->trace_step >= 0) {
+        const size_t len = (size_t)((N + P - 1) / P) * NW * TRACE_SLOTS;
+        if (h->trace_len < len) {
+            if (h->trace) HIPCHK(h, hipFree(h->trace));
+            HIPCHK(h, hipMalloc(&h->trace, len * 8));
+            h->trace_len = len;
+        }
+        HIPCHK(h, hipMemsetAsync(h->trace, 0, len * 8, st));
+    }
+    a.trace = h->trace_step >= 0 ? h->trace : nullptr;
+    a.trace_step = h->trace_step;
+#endif
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     else
-        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return DPK_OK;
@@ -1668,9 +1647,9 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_POSE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_POSE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     else
-        hipLaunchKernelGGL((sample_kernel<M_POSE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a);
+        hipLaunchKernelGGL((sample_kernel<M_POSE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;
@@ -1713,5 +1692,17 @@ int dpk_ddim_update(dpk_handle* h, const float* xt, const float* et, float* xn, 
     HIPCHK(h, hipGetLastError());
     return DPK_OK;
 }
+
+#if DPK_TRACE
+// trace builds only (not part of the C ABI): choose the traced step; copy the stamps out
+int dpk_debug_trace(dpk_handle* h, int step, unsigned long long* out, long long cap) {
+    if (!h) return DPK_E_INVALID;
+    h->trace_step = step;
+    if (!out || !h->trace) return DPK_OK;
+    HIPCHK(h, hipDeviceSynchronize());
+    HIPCHK(h, hipMemcpy(out, h->trace, std::min((size_t)cap, h->trace_len) * 8, hipMemcpyDeviceToHost));
+    return (int)std::min((size_t)cap, h->trace_len);
+}
+#endif
 
 }  // extern "C"
