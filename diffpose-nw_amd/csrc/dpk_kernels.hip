@@ -35,6 +35,10 @@
 #ifndef DPK_TRACE
 #define DPK_TRACE 0
 #endif
+// GEMM phase stamps for tools/gemm_probe.hip (empty in the library)
+#ifndef DPK_GEMM_HOOK
+#define DPK_GEMM_HOOK(tag)
+#endif
 #ifndef DPK_EXP
 #define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
 #endif
@@ -68,7 +72,8 @@ constexpr int SM_XS = 0;                    // residual stream   [R][LDX]
 constexpr int SM_B1 = SM_XS + R * LDX;      // 96-wide scratch   [R][LDX]
 constexpr int SM_B2 = SM_B1 + R * LDX;      // 288-wide scratch  [R][LD2]
 constexpr int SM_XST = SM_B2 + R * LD2;     // pose state x_t    [R][5]
-constexpr int SM_FLOATS = SM_XST + ((R * CIN + 3) / 4) * 4;
+constexpr int SM_LNP = SM_XST + ((R * CIN + 3) / 4) * 4;   // LayerNorm gains/shifts of all layers [NL][4][D]
+constexpr int SM_FLOATS = SM_LNP + NL * 4 * D;
 static_assert(SM_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
 // packed-weight blocks: one block = 16 cols x 16 k = 64 lanes x float4
@@ -183,6 +188,12 @@ __device__ __forceinline__ void ddim_elem(const float* cf, float xt, float et, f
     xn = (cf[2] * x0 + cf[3] * z) + cf[4] * et;
 }
 
+// Sum over the 4 lane rows (l, l^16, l^32, l^48), result in every lane.
+__device__ __forceinline__ float sum4rows(float v) {
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
 // Launder a value through an empty asm so LLVM cannot hoist per-thread address math out
 // of the K-step / layer loops of the persistent kernel (hoisted, it stays live across
 // every phase and spills).
@@ -238,7 +249,11 @@ __device__ __forceinline__ BSrc bsrc(const float* Bp, int ct0, int lane) {
 // addresses only), so the tail tiles are local indices 0..NQ-1 for both.
 enum { TM_NONE = 0, TM_VALU = 1, TM_MFMA4 = 2 };
 
-template <int NR, int NCW, int TM, int TR, int KB>
+// TRANS: the MFMA computes the transposed tile (operands swapped: the packed weight fragment
+// is the A operand, the activation fragment the B operand; both registers are unchanged), so
+// lane l ends up with 4 consecutive COLUMNS 4*(l>>4)..+3 of row l&15 and the epilogue moves
+// one 16-byte vector per tile (ds_write_b128 / ds_read_b128) instead of four 4-byte ones.
+template <int NR, int NCW, int TM, int TR, int KB, bool TRANS = true>
 struct GemmTile {
     static constexpr int TA = TM == TM_VALU ? TR : 1;    // tail A fragments per ring slot
     static constexpr int NQ = TM == TM_MFMA4 ? (NCW + 1) / 2 : 1;
@@ -267,7 +282,8 @@ struct GemmTile {
             for (int i = 0; i < NR; ++i)
 #pragma unroll
                 for (int c = 0; c < NCW; ++c)
-                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+                    acc[i][c] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[c][j], a[i][j], acc[i][c], 0, 0, 0)
+                                      : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
             if constexpr (TM == TM_VALU) {
 #pragma unroll
                 for (int c = 0; c < NCW; ++c)
@@ -275,7 +291,7 @@ struct GemmTile {
                     for (int r = 0; r < TR; ++r) tl[c][r] = fmaf(t[r][j], b[c][j], tl[c][r]);
             } else if constexpr (TM == TM_MFMA4) {
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(t[0][j], b[q][j], tacc[q], 0, 0, 0);
+                for (int q = 0; q < NQ; ++q) tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(b[q][j], t[0][j], tacc[q], 0, 0, 0);
             }
         }
     }
@@ -397,12 +413,27 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         const int cc = c + rot;
         gcol[c] = ct0 + (cc >= NCW ? cc - NCW : cc);
     }
-    float bcol[NCW], tcol[NCW];
+    // bias (and sample-mode temb projection) of this lane's 4 output columns per tile
+    f32x4 bias4[NCW], tp4[NCW];
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
-        const int col = gcol[c] * 16 + rl;
-        bcol[c] = MODE == E_STORE_NB ? 0.f : e.bias[col];
-        tcol[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
+        const int col4 = gcol[c] * 16 + kq;
+        bias4[c] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
+        tp4[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
+                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // tail tiles (TM_MFMA4): lane l holds tail row l&3, columns 4*((l>>2)&3)..+3
+    const int tq4 = 4 * ((lane >> 2) & 3);
+    f32x4 tbias4[NQ], ttp4[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        tbias4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ttp4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (TM == TM_MFMA4) {
+            const int col4 = gcol[q] * 16 + tq4;
+            if (MODE != E_STORE_NB) tbias4[q] = *reinterpret_cast<const f32x4*>(e.bias + col4);
+            if (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ttp4[q] = *reinterpret_cast<const f32x4*>(e.tproj + col4);
+        }
     }
     const BSrc src = bsrc<NC, KB>(Bp, ct0, lane);
     int soff[NCW];
@@ -413,6 +444,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         b0[c] = pre.b0[c];
         b1[c] = pre.b1[c];
     }
+    DPK_GEMM_HOOK(0);
     g.loadA(a0, t0, A, 0);
     if constexpr (KB == 1) {
         g.mma(a0, t0, b0);
@@ -432,72 +464,59 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         g.mma(a0, t0, b0);
         g.mma(a1, t1, b1);
     }
-    float* d = e.dst + ((rt0 * 16 + kq) * e.ldd + rl);
-    float old[NR][NCW][4];
-    if constexpr (MODE == E_RESID || MODE == E_RESID_RELU) {
+    DPK_GEMM_HOOK(1);
+    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
+    auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
+        if constexpr (MODE != E_CHEB1) return f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e.tproj_pose_stride == 0) return uniform4;
+        const int pose = min(e.pose0 + row / J, e.pose_max);
+        return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
+    };
+    f32x4 old[NR][NCW];
+    if constexpr (RES) {
 #pragma unroll
         for (int i = 0; i < NR; ++i)
 #pragma unroll
             for (int c = 0; c < NCW; ++c)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) old[i][c][r] = d[(i * 16 + r) * e.ldd + gcol[c] * 16];
+                old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
     }
 #pragma unroll
-    for (int i = 0; i < NR; ++i)
+    for (int i = 0; i < NR; ++i) {
+        const int row = (rt0 + i) * 16 + rl;
 #pragma unroll
-        for (int c = 0; c < NCW; ++c)
+        for (int c = 0; c < NCW; ++c) {
+            const int col4 = gcol[c] * 16 + kq;
+            const f32x4 tp = tproj4(row, col4, tp4[c]);
+            f32x4 v;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = (rt0 + i) * 16 + kq + r;
-                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[c] * 16 + rl, tcol[c]) : 0.f;
-                d[(i * 16 + r) * e.ldd + gcol[c] * 16] = epi_value<MODE>(
-                    g.acc[i][c][r], bcol[c], tp, (MODE == E_RESID || MODE == E_RESID_RELU) ? old[i][c][r] : 0.f);
-            }
+            for (int r = 0; r < 4; ++r)
+                v[r] = epi_value<MODE>(g.acc[i][c][r], bias4[c][r], tp[r], RES ? old[i][c][r] : 0.f);
+            *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
+        }
+    }
     const int grp = lane >> 4;
     if constexpr (TM == TM_VALU) {
-        float tv[NCW][TR];
-#pragma unroll
-        for (int c = 0; c < NCW; ++c)
-#pragma unroll
-            for (int r = 0; r < TR; ++r) {
-                float v = g.tl[c][r];
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
-                tv[c][r] = v;
-            }
-        if (grp < TR) {
-            const int row = trow0 + grp;
-            float* dt = e.dst + row * e.ldd + rl;
-#pragma unroll
-            for (int c = 0; c < NCW; ++c) {
-                float v = tv[c][0];
-#pragma unroll
-                for (int r = 1; r < TR; ++r)
-                    if (grp == r) v = tv[c][r];
-                const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[gcol[c] * 16] : 0.f;
-                const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[c] * 16 + rl, tcol[c]) : 0.f;
-                dt[gcol[c] * 16] = epi_value<MODE>(v, bcol[c], tp, old_t);
-            }
-        }
+        static_assert(TM != TM_VALU, "gemm_wave computes transposed tiles; VALU tails are gemm_out's");
     } else if constexpr (TM == TM_MFMA4) {
-        // reduce the 4 k-slices; lane group g then writes tail row trow0 + g
-        const int row = trow0 + grp;
-        float* dt = e.dst + row * e.ldd + rl;
+        // reduce the 4 k-slices; lanes 0..15 then hold tail row l&3, columns tq4..tq4+3 of tile q
+        const int row = trow0 + (lane & 3);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             f32x4 v = g.tacc[q];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                v[r] += __shfl_xor(v[r], 16, 64);
-                v[r] += __shfl_xor(v[r], 32, 64);
-            }
-            const float x = grp == 0 ? v[0] : grp == 1 ? v[1] : grp == 2 ? v[2] : v[3];
-            if (q == NQ - 1 && tail_dup) continue;   // duplicate tile (odd NCW, second wave)
-            const float old_t = (MODE == E_RESID || MODE == E_RESID_RELU) ? dt[gcol[q] * 16] : 0.f;
-            const float tp = MODE == E_CHEB1 ? tproj_at(e, row, gcol[q] * 16 + rl, tcol[q]) : 0.f;
-            dt[gcol[q] * 16] = epi_value<MODE>(x, bcol[q], tp, old_t);
+            for (int r = 0; r < 4; ++r) v[r] = sum4rows(v[r]);
+            if (grp != 0 || (q == NQ - 1 && tail_dup)) continue;   // duplicate tile: odd NCW, second wave
+            const int col4 = gcol[q] * 16 + tq4;
+            f32x4* dp = reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4);
+            const f32x4 oldt = RES ? *dp : f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4 tp = tproj4(row, col4, ttp4[q]);
+            f32x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = epi_value<MODE>(v[r], tbias4[q][r], tp[r], oldt[r]);
+            *dp = o;
         }
     }
+    DPK_GEMM_HOOK(2);
 }
 
 // Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
@@ -528,7 +547,7 @@ __device__ __forceinline__ BPre<1> out_prefetch(const float* Bp, int lane) {
 template <int KB, class Epi>
 __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* Bp, int wave, int lane, Epi epi,
                                          const BPre<1>& pre) {
-    using T = GemmTile<1, 1, TM_VALU, 1, KB>;
+    using T = GemmTile<1, 1, TM_VALU, 1, KB, false>;
     static_assert(KB % 2 == 0, "k-blocks in pairs");
     lane = opaque(lane);
     T g;
@@ -553,9 +572,7 @@ __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* B
     }
     g.mma(a0, t0, b0);
     g.mma(a1, t1, b1);
-    float tv = g.tl[0][0];
-    tv += __shfl_xor(tv, 16, 64);
-    tv += __shfl_xor(tv, 32, 64);
+    const float tv = sum4rows(g.tl[0][0]);
     if (rl < COUT) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) epi(wave * 16 + kq + r, rl, g.acc[0][0][r]);
@@ -576,8 +593,8 @@ __device__ __forceinline__ float div_by(float x, float d, float r) {
 // part, part+3, ..., part+21 (interleaved, so the three lanes of a row hit different LDS
 // banks).  Two-pass fp32 statistics, pairwise sums combined in the same order in all three
 // lanes (bitwise identical mean/std per row).
-__device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* __restrict__ gain,
-                                           const float* __restrict__ shift, int tid) {
+__device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
+                                           int tid) {
     tid = opaque(tid);
     const int w = tid >> 6, lane = tid & 63;
     const int row = w * 21 + lane / 3, part = lane % 3;
@@ -622,109 +639,148 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
 }
 
 // 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
-// projections).  16 lanes per (pose, head): lane q owns query q (scores, softmax and P.V in
-// registers, packed fp32 FMAs); query 16 is computed cooperatively by the 16 lanes (one key
-// each, group reductions by shuffles).
+// projections).  One DPP row (16 lanes) per (pose, head); lane q owns query q AND key/value
+// row q in registers.  Keys/values 0..15 reach the other lanes of the row by DPP row_newbcast
+// fused into the FMA (v_fmac_f32_dpp), so the K/V rows are read from LDS once per lane instead
+// of once per (query, key).  Row 16 (key/value 16) is read by every lane of the row; query 16
+// is computed cooperatively (lane j scores key j; lane q sums value column q over the keys).
+template <int J>
+__device__ __forceinline__ void fmac_bcast(float& acc, float row_src, float x) {
+    // acc += row_src[lane J of this 16-lane row] * x
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc)
+        : "v"(row_src), "v"(x), "i"(J));
+}
+
+template <int J>
+__device__ __forceinline__ float row_ror(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
+                                                                 0x120 + J, 0xf, 0xf, false));
+}
+// all-reduce over the 16 lanes of a DPP row
+__device__ __forceinline__ float row_max(float v) {
+    v = fmaxf(v, row_ror<8>(v));
+    v = fmaxf(v, row_ror<4>(v));
+    v = fmaxf(v, row_ror<2>(v));
+    return fmaxf(v, row_ror<1>(v));
+}
+__device__ __forceinline__ float row_sum(float v) {
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    return v + row_ror<1>(v);
+}
+
+// one feature d of this lane's query against keys 0..15 (key rows broadcast from their owner
+// lanes); 16 independent accumulators per instruction group
+template <int J>
+__device__ __forceinline__ void score_keys_d(float (&sc)[16], float kd, float qd) {
+    fmac_bcast<J>(sc[J], kd, qd);
+    if constexpr (J + 1 < 16) score_keys_d<J + 1>(sc, kd, qd);
+}
+template <int J>
+__device__ __forceinline__ void pv_keys(float (&o)[DK], const float (&vr)[DK], const float (&p)[17]) {
+#pragma unroll
+    for (int d = 0; d < DK; ++d) fmac_bcast<J>(o[d], vr[d], p[J]);
+    if constexpr (J + 1 < 16) pv_keys<J + 1>(o, vr, p);
+}
+template <int J>
+__device__ __forceinline__ void pv16_keys(float& o, float pj_row, const float* vcol) {
+    fmac_bcast<J>(o, pj_row, vcol[J * LD2]);
+    if constexpr (J + 1 < 16) pv16_keys<J + 1>(o, pj_row, vcol);
+}
+
 __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
     tid = opaque(tid);
     const int grp = tid >> 4, q = tid & 15;
     const int p = grp >> 2, h = grp & 3;
     const float* rows = qkv + p * J * LD2 + h * DK;     // row i: + i*LD2; K at +D, V at +2D
     float* orows = out + p * J * LDX + h * DK;
+    const float rcp_sdk = 1.0f / SQRT_DK;
     auto keyok = [&](int j) { return ((mask >> j) & 1u) != 0u; };
-    // ---- query q
+    float qr[DK], kr[DK], vr[DK], k16[DK], v16[DK];
+#pragma unroll
+    for (int d = 0; d < DK; d += 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(rows + q * LD2 + d);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(rows + q * LD2 + D + d);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(rows + q * LD2 + 2 * D + d);
+        const f32x4 e = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + D + d);
+        const f32x4 f = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + 2 * D + d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            qr[d + i] = a[i];
+            kr[d + i] = b[i];
+            vr[d + i] = c[i];
+            k16[d + i] = e[i];
+            v16[d + i] = f[i];
+        }
+    }
+    // ---- query q: scores (scaled by division, GraFormer.py:104), softmax, P.V
+    float sc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sc[j] = 0.f;
+#pragma unroll
+    for (int d = 0; d < DK; ++d) score_keys_d<0>(sc, kr[d], qr[d]);
+    float s16 = 0.f;
+#pragma unroll
+    for (int d = 0; d < DK; ++d) s16 = fmaf(qr[d], k16[d], s16);
+    float pr[17];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const float dot = j < 16 ? sc[j] : s16;
+        pr[j] = keyok(j) ? div_by(dot, SQRT_DK, rcp_sdk) : -1e9f;
+        m = fmaxf(m, pr[j]);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        pr[j] = expf(pr[j] - m);
+        sum += pr[j];
+    }
+    const float rs = 1.0f / sum;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) pr[j] = div_by(pr[j], sum, rs);
+    float o[DK];
+#pragma unroll
+    for (int d = 0; d < DK; ++d) o[d] = 0.f;
+    pv_keys<0>(o, vr, pr);
+#pragma unroll
+    for (int d = 0; d < DK; ++d) o[d] = fmaf(pr[16], v16[d], o[d]);
+#pragma unroll
+    for (int d = 0; d < DK; d += 4)
+        *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+    // ---- query 16: lane j scores key j (its own key row); key 16 by every lane
     {
-        f32x2 qv[DK / 2];
+        float a16 = 0.f, b16 = 0.f;
 #pragma unroll
         for (int d = 0; d < DK; d += 4) {
-            const f32x4 t = *reinterpret_cast<const f32x4*>(rows + q * LD2 + d);
-            qv[d / 2] = f32x2{t[0], t[1]};
-            qv[d / 2 + 1] = f32x2{t[2], t[3]};
-        }
-        float sc[J];
-        float m = -INFINITY;
+            const f32x4 qv = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + d);
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const float* kr = rows + j * LD2 + D;
-            f32x2 dot2 = {0.f, 0.f};
-#pragma unroll
-            for (int d = 0; d < DK; d += 4) {
-                const f32x4 t = *reinterpret_cast<const f32x4*>(kr + d);
-                dot2 = pfma(qv[d / 2], f32x2{t[0], t[1]}, dot2);
-                dot2 = pfma(qv[d / 2 + 1], f32x2{t[2], t[3]}, dot2);
-            }
-            const float dot = dot2.x + dot2.y;
-            sc[j] = keyok(j) ? dot / SQRT_DK : -1e9f;
-            m = fmaxf(m, sc[j]);
-        }
-        float sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            sc[j] = expf(sc[j] - m);
-            sum += sc[j];
-        }
-        const float inv = 1.0f / sum;
-        f32x2 o[DK / 2];
-#pragma unroll
-        for (int d = 0; d < DK / 2; ++d) o[d] = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const f32x2 pj = splat2(sc[j] * inv);
-            const float* vr = rows + j * LD2 + 2 * D;
-#pragma unroll
-            for (int d = 0; d < DK; d += 4) {
-                const f32x4 t = *reinterpret_cast<const f32x4*>(vr + d);
-                o[d / 2] = pfma(pj, f32x2{t[0], t[1]}, o[d / 2]);
-                o[d / 2 + 1] = pfma(pj, f32x2{t[2], t[3]}, o[d / 2 + 1]);
+            for (int i = 0; i < 4; ++i) {
+                a16 = fmaf(qv[i], kr[d + i], a16);
+                b16 = fmaf(qv[i], k16[d + i], b16);
             }
         }
-#pragma unroll
-        for (int d = 0; d < DK; d += 4)
-            *reinterpret_cast<f32x4*>(orows + q * LDX + d) =
-                f32x4{o[d / 2].x, o[d / 2].y, o[d / 2 + 1].x, o[d / 2 + 1].y};
-    }
-    // ---- query 16: lane q scores key q (lane 0's key-16 score broadcast)
-    {
-        const float* q16 = rows + 16 * LD2;
-        auto score = [&](int j) {
-            const float* kr = rows + j * LD2 + D;
-            f32x2 dot2 = {0.f, 0.f};
-#pragma unroll
-            for (int d = 0; d < DK; d += 4) {
-                const f32x4 a4 = *reinterpret_cast<const f32x4*>(q16 + d);
-                const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + d);
-                dot2 = pfma(f32x2{a4[0], a4[1]}, f32x2{k4[0], k4[1]}, dot2);
-                dot2 = pfma(f32x2{a4[2], a4[3]}, f32x2{k4[2], k4[3]}, dot2);
-            }
-            const float dot = dot2.x + dot2.y;
-            return keyok(j) ? dot / SQRT_DK : -1e9f;
-        };
-        const float sq = score(q);
-        const float s16 = __shfl(score(16), 0, 16);
-        float m = fmaxf(sq, s16);
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
-        const float eq = expf(sq - m), e16 = expf(s16 - m);
-        float sum = eq;
-#pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 16);
-        sum += e16;
-        const float inv = 1.0f / sum;
-        const float pq = eq * inv, p16 = e16 * inv;
-        float o0 = 0.f, o1 = 0.f;
+        const float sq = keyok(q) ? div_by(a16, SQRT_DK, rcp_sdk) : -1e9f;
+        const float sk = keyok(16) ? div_by(b16, SQRT_DK, rcp_sdk) : -1e9f;
+        const float mm = fmaxf(row_max(sq), sk);
+        const float eq = expf(sq - mm), ek = expf(sk - mm);
+        const float ss = row_sum(eq) + ek;
+        const float rss = 1.0f / ss;
+        const float pq = div_by(eq, ss, rss), pk = div_by(ek, ss, rss);
+        // dims q and q+16 of query 16's output: sum_j p_j * V[j][d] with V read from LDS
         const float* vcol = rows + 2 * D;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float pj = __shfl(pq, j, 16);
-            o0 = fmaf(pj, vcol[j * LD2 + q], o0);
-            if (q < 8) o1 = fmaf(pj, vcol[j * LD2 + q + 16], o1);
-        }
-        o0 = fmaf(p16, vcol[16 * LD2 + q], o0);
+        float o0 = 0.f, o1 = 0.f;
+        asm volatile("s_nop 1" ::: "memory");   // VALU write of pq -> DPP read (2 wait states)
+        pv16_keys<0>(o0, pq, vcol + q);
+        o0 = fmaf(pk, vcol[16 * LD2 + q], o0);
         orows[16 * LDX + q] = o0;
-        if (q < 8) {
-            o1 = fmaf(p16, vcol[16 * LD2 + q + 16], o1);
-            orows[16 * LDX + q + 16] = o1;
-        }
+        // all 16 lanes take part (the DPP broadcasts read every lane of the row); lanes q >= 8
+        // read columns past the head (inside the row) and discard them
+        pv16_keys<0>(o1, pq, vcol + q + 16);
+        o1 = fmaf(pk, vcol[16 * LD2 + q + 16], o1);
+        if (q < DK - 16) orows[16 * LDX + q + 16] = o1;
     }
 }
 
@@ -887,6 +943,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
     float* B1 = sm + SM_B1;
     float* B2 = sm + SM_B2;
     float* XST = sm + SM_XST;
+    float* LNP = sm + SM_LNP;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
@@ -905,6 +962,10 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
     } else {
         for (int i = tid; i < R * CIN; i += NT) XST[i] = i < nvalid ? a.x_in[(size_t)pose0 * PE + i] : 0.f;
     }
+    // LayerNorm parameters of every layer, staged once per launch (the per-lane column slices
+    // are not wave-uniform, and as global loads their L2 latency sat on the LN critical path)
+    static_assert(OFF_LN0B == OFF_LN0A + D && OFF_LN1A == OFF_LN0A + 2 * D && OFF_LN1B == OFF_LN0A + 3 * D, "LN block");
+    for (int i = tid; i < NL * 4 * D; i += NT) LNP[i] = W[(i / (4 * D)) * LAYER_FLOATS + OFF_LN0A + i % (4 * D)];
     __syncthreads();
 
     const int K = MODE == M_SAMPLE ? a.K : 1;
@@ -944,7 +1005,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
             // ---- x = x + MHA(LN0(x))   (GraAttenLayer, GraFormer.py:94-95)
             {
                 const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
-                if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN0A, LW + OFF_LN0B, tid);
+                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
                 BAR();
                 if (DPK_RUN(16 | 32)) {
                     const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
@@ -966,7 +1027,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
             //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
             {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
-                if (DPK_RUN(8)) layer_norm(XS, B1, LW + OFF_LN1A, LW + OFF_LN1B, tid);
+                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
                 BAR();
                 if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
                 BAR();

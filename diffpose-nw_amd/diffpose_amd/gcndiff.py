@@ -77,6 +77,7 @@ class _HipModel:
             raise ValueError(f"adj must be ({npts},{npts}), got {self.adj.shape}")
         _lib.check(h, "dpk_set_graph", L.dpk_set_graph(h, _f32p(self.adj)))
         self._mask_key = None
+        self._mask_ref = None
         self._sched_key = None
         self.training = False
 
@@ -129,10 +130,13 @@ class _HipModel:
         _lib.check(self._h, "dpk_set_mask", L.dpk_set_mask(self._h, m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
 
     def _sync_mask(self, mask) -> None:
+        """Upload the key mask when it changed.  Cached by object identity + in-place version;
+        the cached object is kept alive so its id cannot be recycled by a new tensor."""
         key = None if mask is None else (id(mask), getattr(mask, "_version", 0))
-        if key != self._mask_key or key is None:
+        if key is None or key != self._mask_key or mask is not self._mask_ref:
             self.set_mask(mask)
             self._mask_key = key
+            self._mask_ref = mask
 
     def _check_x(self, x, channels: int = 5):
         if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32):

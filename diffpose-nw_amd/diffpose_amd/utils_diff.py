@@ -68,5 +68,6 @@ def _init_schedule_only(obj: HipGCNdiff, device) -> None:
     obj._h = h
     obj.n_pts = N_PTS
     obj._mask_key = None
+    obj._mask_ref = None
     obj._sched_key = None
     obj.training = False

@@ -3,6 +3,19 @@
 // every CU busy, ITER back-to-back calls separated by a workgroup barrier (as in the sampler).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -Iinclude \
 //        tools/gemm_probe.hip -o build/gemm_probe
+#include <hip/hip_runtime.h>
+// per-wave phase accounting: [0] barrier + prefetch + setup, [1] k-loop, [2] epilogue
+__device__ long long g_acc[3][256 * 4];
+__device__ long long g_last[256 * 4];
+__device__ __forceinline__ void probe_stamp(int tag) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long long t = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) {
+        if (g_last[w]) g_acc[tag][w] += t - g_last[w];
+        g_last[w] = t;
+    }
+}
+#define DPK_GEMM_HOOK(tag) do { __builtin_amdgcn_sched_barrier(0); probe_stamp(tag); __builtin_amdgcn_sched_barrier(0); } while (0)
 #include "../diffpose-nw_amd/csrc/dpk_kernels.hip"
 
 using namespace dpk;
@@ -40,15 +53,28 @@ __global__ void __launch_bounds__(NT, 1) probe(const float* W, float* out, long 
 template <int NC, int KB, int TM>
 static void run(const char* name, const float* W, float* out, long long* cyc) {
     const int iters = 200, grid = 256;
-    for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL((probe<NC, KB, TM>), dim3(grid), dim3(NT), 0, 0, W, out, cyc, iters);
+    hipLaunchKernelGGL((probe<NC, KB, TM>), dim3(grid), dim3(NT), 0, 0, W, out, cyc, iters);
     hipDeviceSynchronize();
+    static long long zeros[3 * 1024 + 1024];
+    hipMemcpyToSymbol(HIP_SYMBOL(g_acc), zeros, sizeof(long long) * 3 * 1024);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_last), zeros, sizeof(long long) * 1024);
+    hipLaunchKernelGGL((probe<NC, KB, TM>), dim3(grid), dim3(NT), 0, 0, W, out, cyc, iters);
+    hipDeviceSynchronize();
+    static long long acc[3 * 1024];
+    hipMemcpyFromSymbol(acc, HIP_SYMBOL(g_acc), sizeof(acc));
+    double ph[3] = {0, 0, 0};
+    for (int t = 0; t < 3; ++t) {
+        for (int i = 0; i < 1024; ++i) ph[t] += acc[t * 1024 + i];
+        ph[t] /= 1024.0 * iters;
+    }
     long long c[256];
     hipMemcpy(c, cyc, sizeof(c), hipMemcpyDeviceToHost);
     double s = 0;
     for (int i = 0; i < grid; ++i) s += c[i];
     const double per = s / grid / iters;
     const double ideal = 2.0 * (NC / 2) * 4 * KB * 32;
-    printf("%-22s NC=%2d KB=%2d TM=%d: %8.0f cyc/call  ideal %6.0f  ratio %.2f\n", name, NC, KB, TM, per, ideal, per / ideal);
+    printf("%-22s NC=%2d KB=%2d TM=%d: %8.0f cyc/call  ideal %6.0f  ratio %.2f | pre+bar %6.0f loop %6.0f epi %6.0f\n", name, NC,
+           KB, TM, per, ideal, per / ideal, ph[0], ph[1], ph[2]);
 }
 
 int main() {
@@ -61,7 +87,6 @@ int main() {
     hipMalloc(&cyc, 256 * 8);
     for (int tm = 0; tm < 3; ++tm) {
         if (tm == 0) { run<18, 6, 0>("QKV", W, out, cyc); run<12, 6, 0>("fc1", W, out, cyc); run<6, 12, 0>("fc2", W, out, cyc); run<6, 18, 0>("C1/C2", W, out, cyc); run<6, 6, 0>("O", W, out, cyc); }
-        if (tm == 1) { run<18, 6, 1>("QKV", W, out, cyc); run<12, 6, 1>("fc1", W, out, cyc); run<6, 12, 1>("fc2", W, out, cyc); run<6, 18, 1>("C1/C2", W, out, cyc); run<6, 6, 1>("O", W, out, cyc); }
         if (tm == 2) { run<18, 6, 2>("QKV", W, out, cyc); run<12, 6, 2>("fc1", W, out, cyc); run<6, 12, 2>("fc2", W, out, cyc); run<6, 18, 2>("C1/C2", W, out, cyc); run<6, 6, 2>("O", W, out, cyc); }
     }
     return 0;
