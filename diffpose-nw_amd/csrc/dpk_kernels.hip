@@ -16,6 +16,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -35,7 +36,29 @@
 #ifndef DPK_TRACE
 #define DPK_TRACE 0
 #endif
-// GEMM phase stamps for tools/gemm_probe.hip (empty in the library)
+// GEMM phase stamps: tools/gemm_probe.hip defines its own; trace builds stamp into the trace
+// buffer (end of k-loop, end of epilogue); empty in the library
+#if DPK_TRACE
+namespace dpk {
+__shared__ unsigned long long* tr_row[4];   // per-wave stamp row of the traced step (null: off)
+__shared__ int tr_ix[4];
+__device__ __forceinline__ void tr_stamp() {
+    const int w = threadIdx.x >> 6;
+    if (tr_row[w] && (threadIdx.x & 63) == 0 && tr_ix[w] < 256) tr_row[w][tr_ix[w]] = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0 && tr_row[w]) tr_ix[w] += 1;
+}
+}  // namespace dpk
+#ifndef DPK_GEMM_HOOK
+#define DPK_GEMM_HOOK(tag)                       \
+    do {                                         \
+        if ((tag) != 0) {                        \
+            __builtin_amdgcn_sched_barrier(0);   \
+            dpk::tr_stamp();                     \
+            __builtin_amdgcn_sched_barrier(0);   \
+        }                                        \
+    } while (0)
+#endif
+#endif
 #ifndef DPK_GEMM_HOOK
 #define DPK_GEMM_HOOK(tag)
 #endif
@@ -60,8 +83,13 @@ constexpr int COUT = 5;      // coords_dim[1]
 constexpr int PE = J * CIN;  // floats per pose (85)
 
 // workgroup tile
-constexpr int P = 4;         // poses per workgroup
-constexpr int R = P * J;     // 68 rows
+#ifndef DPK_P
+#define DPK_P 4              // poses per workgroup: 4 (one workgroup per CU) or 2 (two per CU)
+#endif
+constexpr int P = DPK_P;     // poses per workgroup
+constexpr int R = P * J;     // 68 (34) rows
+static_assert(P == 4 || P == 2, "4 or 2 poses per workgroup");
+constexpr int WG_PER_CU = P == 4 ? 1 : 2;
 constexpr int NT = 256;      // threads (4 waves, one per SIMD)
 constexpr int NW = NT / 64;
 constexpr int LDX = 104;     // LDS row stride, 96-wide buffers  (≡40 mod 64: conflict-free b128 A reads)
@@ -148,6 +176,7 @@ struct SampleArgs {
     unsigned mask;        // 17-bit key mask
     float eta;
     unsigned long long seed;
+    int phase_delay;      // two workgroups per CU: start delay (cycles) of the grid's second half
 #if DPK_TRACE
     unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
     int trace_step;
@@ -188,10 +217,18 @@ __device__ __forceinline__ void ddim_elem(const float* cf, float xt, float et, f
     xn = (cf[2] * x0 + cf[3] * z) + cf[4] * et;
 }
 
-// Sum over the 4 lane rows (l, l^16, l^32, l^48), result in every lane.
+// Sum over the 4 lane rows (l, l^16, l^32, l^48), result in every lane, on the VALU: a
+// v_permlane32_swap / v_permlane16_swap of two copies of v leaves (v, partner) split across
+// the two registers, so their sum is v + partner in every lane (tools/permlane_probe.hip; the
+// clang builtins return a mis-assigned pair on this toolchain, hence the inline asm).  Replaces
+// two LDS-crossbar shuffles.
 __device__ __forceinline__ float sum4rows(float v) {
-    v += __shfl_xor(v, 16, 64);
-    return v + __shfl_xor(v, 32, 64);
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    const float s1 = a + b;
+    float c = s1, d = s1;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+    return c + d;
 }
 
 // Launder a value through an empty asm so LLVM cannot hoist per-thread address math out
@@ -307,9 +344,15 @@ struct BPre {
     f32x4 b0[NCW], b1[NCW];
 };
 
+// Wave roles in the workgroup GEMM: column half ch(w) and index within the pair of waves that
+// share it, pr(w).  68 rows: wave w = row tiles 2*(w>>1)+{0,1} of column half w&1; 34 rows:
+// row tile w&1 of column half w>>1.
+__device__ __forceinline__ int gemm_ch(int wave) { return R == 68 ? (wave & 1) : (wave >> 1); }
+__device__ __forceinline__ int gemm_pr(int wave) { return R == 68 ? (wave >> 1) : (wave & 1); }
+
 // Column rotation of wave `wave` within its column half (TM_MFMA4 tail split, see GemmTile).
 template <int NCW>
-__device__ __forceinline__ int col_rot(int wave) { return (wave >> 1) ? (NCW + 1) / 2 : 0; }
+__device__ __forceinline__ int col_rot(int wave) { return gemm_pr(wave) ? (NCW + 1) / 2 : 0; }
 
 // SGPR byte offsets of the wave's NCW column tiles' first k-block, rotation applied.
 template <int NCW, int KB>
@@ -324,7 +367,7 @@ __device__ __forceinline__ void tile_offsets(int (&soff)[NCW], int sbase, int ro
 template <int NC, int KB>
 __device__ __forceinline__ BPre<NC / 2> gemm_prefetch(const float* Bp, int wave, int lane) {
     constexpr int NCW = NC / 2;
-    const BSrc s = bsrc<NC, KB>(Bp, (wave & 1) * NCW, lane);
+    const BSrc s = bsrc<NC, KB>(Bp, gemm_ch(wave) * NCW, lane);
     int soff[NCW];
     tile_offsets<NCW, KB>(soff, s.sbase, col_rot<NCW>(wave));
     BPre<NCW> pre;
@@ -438,32 +481,36 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     const BSrc src = bsrc<NC, KB>(Bp, ct0, lane);
     int soff[NCW];
     tile_offsets<NCW, KB>(soff, src.sbase, rot);
-    f32x4 a0[NR], t0[TA], b0[NCW], a1[NR], t1[TA], b1[NCW];
+    // S-stage register ring: slot st holds k-block kb+st; its refill (k-block kb+st+S) is issued
+    // right after its MFMAs, so loads run S-1 slots ahead of use.  3 slots where a slot is
+    // short (NCW <= 6: 24-48 MFMAs, below the loaded L2 latency), 2 for the 9-tile QKV halves.
+    constexpr int S = (KB == 1) ? 1 : (NCW <= 6 && KB % 3 == 0) ? 3 : 2;
+    static_assert(KB == 1 || KB % S == 0, "ring slots divide the k-blocks");
+    f32x4 as[S][NR], ts[S][TA], bs[S][NCW];
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
-        b0[c] = pre.b0[c];
-        b1[c] = pre.b1[c];
+        bs[0][c] = pre.b0[c];
+        if constexpr (S > 1) bs[1][c] = pre.b1[c];
     }
     DPK_GEMM_HOOK(0);
-    g.loadA(a0, t0, A, 0);
-    if constexpr (KB == 1) {
-        g.mma(a0, t0, b0);
-    } else {
-        g.loadA(a1, t1, A, 1);
+#pragma unroll
+    for (int st = 2; st < S; ++st) T::loadB(bs[st], src, soff, st);
+#pragma unroll
+    for (int st = 0; st < S; ++st) g.loadA(as[st], ts[st], A, st);
+    if constexpr (KB > S) {
 #pragma unroll 1
-        for (int kb = 0; kb < KB - 2; kb += 2) {
-            g.mma(a0, t0, b0);
-            T::loadB(b0, src, soff, kb + 2);
-            g.loadA(a0, t0, A, kb + 2);
-            T::schedule_half();
-            g.mma(a1, t1, b1);
-            T::loadB(b1, src, soff, kb + 3);
-            g.loadA(a1, t1, A, kb + 3);
-            T::schedule_half();
+        for (int kb = 0; kb < KB - S; kb += S) {
+#pragma unroll
+            for (int st = 0; st < S; ++st) {
+                g.mma(as[st], ts[st], bs[st]);
+                T::loadB(bs[st], src, soff, kb + st + S);
+                g.loadA(as[st], ts[st], A, kb + st + S);
+                T::schedule_half();
+            }
         }
-        g.mma(a0, t0, b0);
-        g.mma(a1, t1, b1);
     }
+#pragma unroll
+    for (int st = 0; st < S; ++st) g.mma(as[st], ts[st], bs[st]);
     DPK_GEMM_HOOK(1);
     constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
     auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
@@ -505,7 +552,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
             f32x4 v = g.tacc[q];
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = sum4rows(v[r]);
-            if (grp != 0 || (q == NQ - 1 && tail_dup)) continue;   // duplicate tile: odd NCW, second wave
+            if (grp != 0 || (q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
             const int col4 = gcol[q] * 16 + tq4;
             f32x4* dp = reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4);
             const f32x4 oldt = RES ? *dp : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -525,12 +572,13 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
 template <int NC, int KB, int MODE>
 __device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp, int wave, int lane,
                                         const EpiArgs& e, const BPre<NC / 2>& pre) {
-    static_assert(NC % 2 == 0 && R == 68 && NW == 4, "4 row tiles x 2 column halves + 4 tail rows");
+    static_assert(NC % 2 == 0 && (R == 68 || R == 34) && NW == 4, "row tiles x 2 column halves + tail rows");
     constexpr int NCW = NC / 2;
-    const int half = wave >> 1;
-    const bool dup = (NCW & 1) && half == 1;
-    gemm_wave<2, NCW, TM_MFMA4, 0, NC, KB, MODE>(A, lda, Bp, 2 * half, (wave & 1) * NCW, col_rot<NCW>(wave), 64, dup,
-                                                 lane, e, pre);
+    constexpr int NRW = R == 68 ? 2 : 1;            // row tiles per wave
+    const int pr = gemm_pr(wave);
+    const bool dup = (NCW & 1) && pr == 1;
+    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW, col_rot<NCW>(wave),
+                                                   R - R % 16, dup, lane, e, pre);
 }
 
 // Output ChebConv (96->5, one col tile): waves 0-3, wave w = row tile w + tail row 64+w; the
@@ -555,7 +603,7 @@ __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* B
     g.tl[0][0] = 0.f;
     const int rl = lane & 15, kq = (lane >> 4) * 4;
     g.aoff[0] = (wave * 16 + rl) * lda + kq;
-    g.toff[0] = (64 + wave) * lda + kq;
+    g.toff[0] = (R - R % 16 + wave) * lda + kq;
     const BSrc src = bsrc<1, KB>(Bp, 0, lane);
     const int soff[1] = {0};
     f32x4 a0[1], t0[1], b0[1] = {pre.b0[0]}, a1[1], t1[1], b1[1] = {pre.b1[0]};
@@ -576,7 +624,7 @@ __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* B
     if (rl < COUT) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) epi(wave * 16 + kq + r, rl, g.acc[0][0][r]);
-        if (kq == 0) epi(64 + wave, rl, tv);
+        if (kq == 0) epi(R - R % 16 + wave, rl, tv);
     }
 }
 // ---------------------------------------------------------------------------------------
@@ -694,6 +742,7 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
     tid = opaque(tid);
     const int grp = tid >> 4, q = tid & 15;
     const int p = grp >> 2, h = grp & 3;
+    if (p >= P) return;                                 // whole DPP rows (34-row tiles: waves 2-3)
     const float* rows = qkv + p * J * LD2 + h * DK;     // row i: + i*LD2; K at +D, V at +2D
     float* orows = out + p * J * LDX + h * DK;
     const float rcp_sdk = 1.0f / SQRT_DK;
@@ -935,7 +984,7 @@ template <int MODE, bool SPARSE>
 // is never written during the launch and turns its wave-uniform loads (Laplacians, Chebyshev
 // terms, LayerNorm gains, biases) into scalar s_load (in the SampleArgs struct it cannot, and
 // every such value became a vector load with its L2 latency exposed).
-__global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float* __restrict__ arena) {
+__global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, const float* __restrict__ arena) {
     constexpr bool EPS_MODE = MODE == M_EPS;
     constexpr bool POSE = MODE == M_POSE;
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
@@ -966,17 +1015,27 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
     // are not wave-uniform, and as global loads their L2 latency sat on the LN critical path)
     static_assert(OFF_LN0B == OFF_LN0A + D && OFF_LN1A == OFF_LN0A + 2 * D && OFF_LN1B == OFF_LN0A + 3 * D, "LN block");
     for (int i = tid; i < NL * 4 * D; i += NT) LNP[i] = W[(i / (4 * D)) * LAYER_FLOATS + OFF_LN0A + i % (4 * D)];
+    if (WG_PER_CU == 2 && a.phase_delay > 0 && blockIdx.x >= (gridDim.x + 1) / 2) {
+        // de-phase the two co-resident workgroups of a CU so one runs its VALU phases while the
+        // other runs MFMA phases (the dispatcher fills second CU slots with the grid's second half)
+        const long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < a.phase_delay) __builtin_amdgcn_s_sleep(8);
+    }
     __syncthreads();
 
     const int K = MODE == M_SAMPLE ? a.K : 1;
 #if DPK_TRACE
-    int tix = 0;
-    unsigned long long* trow = a.trace ? a.trace + ((size_t)blockIdx.x * NW + wave) * TRACE_SLOTS : nullptr;
-#define DPK_STAMP()                                                                        \
-    do {                                                                                   \
-        if (trow && s == a.trace_step && (tid & 63) == 0 && tix < TRACE_SLOTS)             \
-            trow[tix] = __builtin_amdgcn_s_memtime();                                      \
-        tix += (trow && s == a.trace_step) ? 1 : 0;                                        \
+    if ((tid & 63) == 0) {
+        tr_row[wave] = nullptr;
+        tr_ix[wave] = 0;
+    }
+#define DPK_STAMP()                                                                                       \
+    do {                                                                                                  \
+        if ((tid & 63) == 0)                                                                              \
+            tr_row[wave] = (a.trace && s == a.trace_step)                                                 \
+                               ? a.trace + ((size_t)blockIdx.x * NW + wave) * TRACE_SLOTS                 \
+                               : nullptr;                                                                 \
+        tr_stamp();                                                                                       \
     } while (0)
 #define BAR()          \
     do {               \
@@ -1103,7 +1162,7 @@ __global__ void __launch_bounds__(NT, 1) sample_kernel(SampleArgs a, const float
                     }
                 }
             };
-            gemm_out<18>(B2, LD2, W + OFF_WOUT, wave, lane, epi, preo);
+            if (wave < R / 16) gemm_out<18>(B2, LD2, W + OFF_WOUT, wave, lane, epi, preo);
         }
         BAR();
     }
@@ -1205,6 +1264,7 @@ using namespace dpk;
 struct dpk_handle {
     int device = 0;
     int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
+    int phase_delay = 0;           // DPK_PHASE_DELAY (cycles), two-workgroups-per-CU builds only
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
@@ -1351,6 +1411,8 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     dpk_handle* h = new dpk_handle();
     h->device = cfg->device;
     h->kind = kind;
+    if (const char* pd = getenv("DPK_PHASE_DELAY")) h->phase_delay = atoi(pd);
+    else h->phase_delay = WG_PER_CU == 2 ? 60000 : 0;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_temb.assign(TEMB_FLOATS, 0.f);
     *out = h;
@@ -1660,6 +1722,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.mask = h->mask;
     a.eta = h->eta;
     a.seed = seed;
+    a.phase_delay = h->phase_delay;
 #if DPK_TRACE
     if (h->trace_step >= 0) {
         const size_t len = (size_t)((N + P - 1) / P) * NW * TRACE_SLOTS;

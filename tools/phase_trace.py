@@ -1,10 +1,10 @@
 """Per-phase cycle breakdown of one DDIM step of the sampler kernel.
 
 Uses a trace build of libdpk (-DDPK_TRACE=1). In that build, lane 0 of every wave stamps
-s_memtime before and after each workgroup barrier of one chosen step. Per phase it reports:
-- wall: the barrier-exit to barrier-exit delta, averaged over workgroups;
-- the slowest and the fastest wave's compute time up to the barrier.
-Each phase type is summed over the 5 layers.
+s_memtime before and after each workgroup barrier of one chosen step, and inside every GEMM at
+the end of its k-loop and of its epilogue. Per phase (summed over the 5 layers) it reports the
+slowest wave's segments, averaged over workgroups: GEMM startup+k-loop, epilogue, VALU compute
+up to the barrier, and the barrier wait.
 
   python tools/phase_trace.py --build     # build container: hipcc -> build/trace/libdpk_trace.so
   python tools/phase_trace.py --run       # GPU box: B=1024, K=50, trace step 10
@@ -19,9 +19,26 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "build", "trace", "libdpk_trace.so")
 
-LAYER = ["LN0", "QKV", "attention", "O", "LN1", "graph1", "fc1", "fc2", "graph2+b2", "cheb_prep1", "C1",
-         "cheb_prep2", "C2"]
-NAMES = ["input_prep", "input_gemm"] + [f"L{l}.{n}" for l in range(5) for n in LAYER] + ["cheb_out", "out_gemm+ddim"]
+# stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
+# ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
+def _events():
+    ev = []
+    bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
+    gemm = lambda n: ev.extend([(n, "loop"), (n, "epi")])
+    bar("input_prep"); gemm("input_gemm"); bar("input_gemm")
+    for l in range(5):
+        p = f"L{l}."
+        bar(p + "LN0"); gemm(p + "QKV"); bar(p + "QKV")
+        bar(p + "attention"); gemm(p + "O"); bar(p + "O")
+        bar(p + "LN1"); bar(p + "graph1"); gemm(p + "fc1"); bar(p + "fc1")
+        gemm(p + "fc2"); bar(p + "fc2")
+        bar(p + "graph2+b2"); bar(p + "cheb_prep1"); gemm(p + "C1"); bar(p + "C1")
+        bar(p + "cheb_prep2"); gemm(p + "C2"); bar(p + "C2")
+    bar("cheb_out"); bar("out_gemm+ddim")
+    return ev
+
+
+EVENTS = _events()
 
 
 def build():
@@ -63,31 +80,31 @@ def run(step=10, frames=1024):
     buf = np.zeros(nblk * 4 * 256, dtype=np.uint64)
     n = L.dpk_debug_trace(m._h, step, buf.ctypes.data, buf.size)
     assert n == buf.size, n
-    t = buf.reshape(nblk, 4, 256).astype(np.int64)
-    nb = len(NAMES)
-    pre = t[:, :, 0:2 * nb:2]          # before barrier p
-    post = t[:, :, 1:2 * nb:2]         # after barrier p
-    assert (pre > 0).all() and (post > 0).all(), "missing stamps"
-    step_cyc = (post[:, :, -1] - post[:, :, 0]).mean()
-    rows = []
-    for p in range(1, nb):
-        wall = (post[:, 0, p] - post[:, 0, p - 1]).mean()
-        comp = pre[:, :, p] - post[:, :, p - 1]
-        rows.append((NAMES[p], wall, comp.max(1).mean(), comp.min(1).mean()))
+    ne = len(EVENTS)
+    t = buf.reshape(nblk, 4, 256)[:, :, :ne].astype(np.int64)
+    assert (t > 0).all(), "missing stamps"
+    d = np.diff(t, axis=2)                      # interval k ends at event k+1
+    step_cyc = float((t[:, :, -1] - t[:, :, 0]).mean())
+    # per phase: compute = previous barrier exit -> this barrier entry (slowest wave), split for
+    # GEMMs into startup+k-loop / epilogue; wait = barrier entry -> exit
     agg = {}
-    for name, wall, cmax, cmin in rows:
-        key = name.split(".", 1)[1] if name.startswith("L") else name
-        a = agg.setdefault(key, [0.0, 0.0, 0.0])
-        a[0] += wall
-        a[1] += cmax
-        a[2] += cmin
-    total = sum(v[0] for v in agg.values())
-    print(f"kernel {ms:.3f} ms for {len(seq)} steps; traced step {step}: {step_cyc:.0f} cycles "
-          f"(sum of phases {total:.0f}); implied clock {step_cyc / (ms / len(seq) * 1e-3) / 1e9:.2f} GHz")
-    print(f"{'phase':<14}{'wall cyc':>10}{'%':>7}{'max wave':>10}{'min wave':>10}")
-    for k, (w, cmax, cmin) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
-        print(f"{k:<14}{w:>10.0f}{100 * w / total:>7.1f}{cmax:>10.0f}{cmin:>10.0f}")
-    print(json.dumps({"step_cycles": float(step_cyc), "phases": {k: [round(v, 1) for v in vals] for k, vals in agg.items()}}))
+    for k in range(ne - 1):
+        name, kind = EVENTS[k + 1]
+        key = name.split(".", 1)[1] if name.startswith("L") and "." in name else name
+        part = {"pre": "compute", "post": "wait", "loop": "loop", "epi": "epilogue"}[kind]
+        if kind == "pre" and EVENTS[k][1] == "epi":
+            part = "after_epi"
+        a = agg.setdefault(key, {})
+        a[part] = a.get(part, 0.0) + float(d[:, :, k].max(1).mean())
+    total = sum(sum(v.values()) for v in agg.values())
+    print(f"kernel {ms:.3f} ms for {len(seq)} steps; traced step {step}: {step_cyc:.0f} cycles (sum of slowest-wave "
+          f"segments {total:.0f}); implied clock {step_cyc / (ms / len(seq) * 1e-3) / 1e9:.2f} GHz")
+    cols = ["loop", "epilogue", "after_epi", "compute", "wait"]
+    print(f"{'phase':<14}" + "".join(f"{c:>11}" for c in cols) + f"{'total':>10}{'%':>7}")
+    for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1].values())):
+        tot = sum(v.values())
+        print(f"{k:<14}" + "".join(f"{v.get(c, 0):>11.0f}" for c in cols) + f"{tot:>10.0f}{100 * tot / total:>7.1f}")
+    print(json.dumps({"step_cycles": step_cyc, "phases": {k: {c: round(x, 1) for c, x in v.items()} for k, v in agg.items()}}))
 
 
 if __name__ == "__main__":
