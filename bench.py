@@ -32,6 +32,7 @@ for _p in (os.path.join(ROOT, "diffpose-nw_amd"), ROOT):
 
 W_ALG = 25_996_254          # FLOP per pose-step, as written (torch FlopCounterMode-verified)
 PEAK_FP32_MFMA = 157.3      # TFLOP/s, MI355X FP32 matrix peak (MI355X_MICROARCH.md, chip table)
+PEAK_F16_MFMA = 2516.6      # TFLOP/s, MI355X dense FP16 matrix peak (16x the f32 rate, same table)
 METRIC = "poses/sec (B=1024, 17j, K=50 DDIM) at 1/2/4/8 MI355X; MPJPE Δ vs ref"
 
 
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=1024)
     ap.add_argument("--cpu-repeats", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gemm", choices=("fp32", "f16x3"), default="fp32",
+                    help="per-layer GEMM arithmetic (dpk_set_gemm_mode); fp32 is the reference's")
     return ap.parse_args()
 
 
@@ -95,6 +98,7 @@ def main():
     # ---- model, schedule, inputs (synthetic, seeded) ----
     model = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
     model.load_state_dict(synthetic_state_dict())
+    model.set_gemm_mode(args.gemm)
     seq = make_seq("uniform", args.T_test, args.K)
     betas = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
                                                num_diffusion_timesteps=args.T)).float()
@@ -154,16 +158,18 @@ def main():
     roof = None
     if avg_kernel_ms:
         achieved = W_ALG * rows * K / (avg_kernel_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_MFMA, 4), "traffic": None,
-                "kernel": "dpk::sample_kernel<0, *>", "avg_launch_ms": round(avg_kernel_ms, 4),
+        # f16x3: every fp32 product is three f16 MFMA passes, so the fp32-equivalent peak is 1/3 of f16's
+        peak = PEAK_FP32_MFMA if args.gemm == "fp32" else round(PEAK_F16_MFMA / 3, 1)
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": "dpk::sample_kernel<0, *, %s>" % ("false" if args.gemm == "fp32" else "true"), "avg_launch_ms": round(avg_kernel_ms, 4),
                 "launches": len(kernel_ms), "flop_per_launch": W_ALG * rows * K,
                 "per_unit": f"{W_ALG} FLOP per pose-step (SURVEY 8d) x {rows} poses x {K} steps"}
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
             try:
                 tr = json.load(open(tfile))
-                key = f"frames{args.frames}_hyp{args.hyp}_K{K}"
+                key = f"frames{args.frames}_hyp{args.hyp}_K{K}" + ("" if args.gemm == "fp32" else "_" + args.gemm)
                 if key in tr:
                     roof["traffic"] = tr[key]["hbm_bytes_per_launch"]
                     roof["traffic_source"] = tr[key]["source"]
@@ -173,13 +179,14 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32",
+        "vs_baseline": None,
+        "dtype": "fp32" if args.gemm == "fp32" else "fp32 (layer GEMMs as 3x fp16-split MFMA, fp32 accumulate)",
         "data": "synthetic: seeded PCG64 Human3.6M-shaped uvxyz poses and GCNdiff weights (no H36M/checkpoints offline)",
         "config": {"workload": f"human36m_diffpose_uvxyz_cpn eval: {args.frames} frames/GPU x H={args.hyp}, "
                                f"K={K} DDIM (uniform skip over T'={args.T_test}, T={args.T}), eta={args.eta}",
                    "frames_per_gpu": args.frames, "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
                    "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if world > 1 else ""),
-                   "hipgraph": bool(args.graph)},
+                   "hipgraph": bool(args.graph), "gemm": args.gemm},
         "roofline": roof,
         "cpu_baseline": None,
     }

@@ -134,6 +134,21 @@ constexpr int OFF_CHEB = OFF_BOUT + 16;                     // dense T1 [17x17] 
 constexpr int OFF_CHEBS = OFF_CHEB + 2 * J * J;             // H36M-sparse T1 (49) then T2 (87) values
 constexpr int ARENA_FLOATS = ((OFF_CHEBS + 136 + 63) / 64) * 64;
 
+// Split-fp16 GEMM arena (gemm mode 1): per layer, each GEMM's weights x W16_SCALE split into
+// fp16 hi + lo parts, packed as 16x16x32 B fragments: block (16 cols x 32 k) = [hi 1 KiB | lo 1 KiB],
+// lane l holding W[k = kb*32 + 8*(l>>4) + i][n = ct*16 + (l&15)] in half i = 0..7.  Byte offsets.
+constexpr float W16_SCALE = 64.0f;            // keeps the lo parts of O(0.01) weights in fp16's normal range
+constexpr int BLK16 = 2048;
+constexpr int KB32_D = D / 32, KB32_D2 = D2 / 32, KB32_D3 = D3 / 32;   // 3, 6, 9
+constexpr int O16_QKV = 0;                                             // [18 ct][3 kb]
+constexpr int O16_O = O16_QKV + 18 * KB32_D * BLK16;                   // [6][3]
+constexpr int O16_FC1 = O16_O + 6 * KB32_D * BLK16;                    // [12][3]
+constexpr int O16_FC2 = O16_FC1 + 12 * KB32_D * BLK16;                 // [6][6]
+constexpr int O16_C1 = O16_FC2 + 6 * KB32_D2 * BLK16;                  // [6][9]
+constexpr int O16_C2 = O16_C1 + 6 * KB32_D3 * BLK16;                   // [6][9]
+constexpr int LAYER16_BYTES = O16_C2 + 6 * KB32_D3 * BLK16;
+constexpr int ARENA16_BYTES = NL * LAYER16_BYTES;
+
 // timestep-MLP arena (transposed nn.Linear weights: [in][out])
 constexpr int TOFF_W0 = 0;                    // [96][384]
 constexpr int TOFF_B0 = TOFF_W0 + D * E;
@@ -152,6 +167,41 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // packed fp32 fma (v_pk_fma_f32: two lanes of work per instruction)
 __device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
+
+// ---- split-fp16 activation layout (gemm mode 1) -------------------------------------------
+// A GEMM input row of K fp32 values is stored as K/8 chunks of 32 bytes: [hi(8 x fp16) | lo(8 x fp16)]
+// with hi = fp16(v), lo = fp16(v - hi).  A lane's 16x16x32 A fragment (8 consecutive k) is then
+// two 16-byte LDS reads, with no conversion in the k-loop.  Same bytes per row as fp32.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split_f16(f32x2 v, f16x2& hi, f16x2& lo) {
+    hi = __builtin_convertvector(v, f16x2);
+    lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x2), f16x2);
+}
+// 4 consecutive columns col..col+3 (col % 4 == 0) of a split row
+__device__ __forceinline__ void split_store4(char* row, int col, f32x4 v) {
+    f16x2 h0, l0, h1, l1;
+    split_f16(f32x2{v[0], v[1]}, h0, l0);
+    split_f16(f32x2{v[2], v[3]}, h1, l1);
+    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
+    *reinterpret_cast<f16x4*>(p) = f16x4{h0[0], h0[1], h1[0], h1[1]};
+    *reinterpret_cast<f16x4*>(p + 16) = f16x4{l0[0], l0[1], l1[0], l1[1]};
+}
+__device__ __forceinline__ void split_store2(char* row, int col, f32x2 v) {   // col % 2 == 0
+    f16x2 h, l;
+    split_f16(v, h, l);
+    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
+    *reinterpret_cast<f16x2*>(p) = h;
+    *reinterpret_cast<f16x2*>(p + 16) = l;
+}
+__device__ __forceinline__ void split_store1(char* row, int col, float v) {
+    const _Float16 h = (_Float16)v;
+    const _Float16 l = (_Float16)(v - (float)h);
+    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
+    *reinterpret_cast<_Float16*>(p) = h;
+    *reinterpret_cast<_Float16*>(p + 16) = l;
+}
 
 // Kernel modes: the K-step sampler (GCNdiff + DDIM), one GCNdiff eps evaluation, or one
 // GCNpose forward (models/gcnpose.py:101-113: the same backbone without the timestep
@@ -581,6 +631,242 @@ __device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp
                                                    R - R % 16, dup, lane, e, pre);
 }
 
+// ---------------------------------------------------------------------------------------
+// Split-fp16 GEMM (gemm mode 1): out = A.W as 3 fp16 MFMA products per tile and k-block,
+// hi(A)hi(W) + hi(A)lo(W) + lo(A)hi(W), accumulated in fp32 (v_mfma_f32_16x16x32_f16; the
+// dropped lo.lo term is ~2^-22 relative).  fp16 x fp16 products are exact in fp32, so the error
+// is that of the two-part split: ~2^-22 per product (fp32 rounding: 2^-24).  5.3x the fp32 MFMA
+// rate (16 cycles per 16x16x32 vs 8 x 32 cycles for the same k on 16x16x4 f32).
+// Weights carry a x64 scale (exact power of two, undone in the epilogue) so their lo parts stay
+// normal fp16.  Same tile geometry as the fp32 path: transposed tiles, 4 tail rows on
+// v_mfma_f32_4x4x4_16b_f16 split between the two waves of a column half; columns in passes of
+// 3 tiles (keeps the hi+lo B ring within the register budget).
+struct BSrc16 {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int voff;
+    __device__ __forceinline__ f16x8 load(int byteoff) const {
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, byteoff, 0));
+    }
+};
+template <int NC, int KB32>
+__device__ __forceinline__ BSrc16 bsrc16(const char* Bp, int lane) {
+    BSrc16 s;
+    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, NC * KB32 * BLK16, 0x00020000);
+    s.voff = lane * 16;
+    return s;
+}
+
+constexpr int PW16 = 3;      // column tiles per pass
+template <int PW>
+struct BPre16 {
+    f16x8 h0[PW], l0[PW], h1[PW], l1[PW];
+};
+
+// global column tile of local tile c of a pass starting at ctp, rotated by rot
+template <int PW>
+__device__ __forceinline__ int pass_col(int ctp, int c, int rot) {
+    const int cc = c + rot;
+    return ctp + (cc >= PW ? cc - PW : cc);
+}
+
+// first two k-blocks of the wave's first pass (issued before the preceding VALU phase)
+template <int NC, int KB32>
+__device__ __forceinline__ BPre16<PW16> gemm16_prefetch(const char* Bp, int wave, int lane) {
+    constexpr int NCW = NC / 2;
+    const BSrc16 s = bsrc16<NC, KB32>(Bp, lane);
+    const int ctp = gemm_ch(wave) * NCW, rot = gemm_pr(wave) ? (PW16 + 1) / 2 : 0;
+    BPre16<PW16> pre;
+#pragma unroll
+    for (int c = 0; c < PW16; ++c) {
+        const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
+        pre.h0[c] = s.load(b0);
+        pre.l0[c] = s.load(b0 + 1024);
+        pre.h1[c] = s.load(b0 + BLK16);
+        pre.l1[c] = s.load(b0 + BLK16 + 1024);
+    }
+    return pre;
+}
+
+__device__ __forceinline__ f16x4 half_lo(f16x8 v) { return __builtin_shufflevector(v, v, 0, 1, 2, 3); }
+__device__ __forceinline__ f16x4 half_hi(f16x8 v) { return __builtin_shufflevector(v, v, 4, 5, 6, 7); }
+
+template <int NR, int PW, int NC, int KB32, int MODE, bool OUTSPLIT>
+__device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16& src, int rt0, int ctp, int rot,
+                                            int trow0, bool tail_dup, int lane, const EpiArgs& e,
+                                            const BPre16<PW>& pre) {
+    constexpr int NQ = (PW + 1) / 2;
+    lane = opaque(lane);
+    const int rl = lane & 15, g = lane >> 4, kq = g * 4;
+    int gcol[PW], soff[PW];
+#pragma unroll
+    for (int c = 0; c < PW; ++c) {
+        gcol[c] = pass_col<PW>(ctp, c, rot);
+        soff[c] = gcol[c] * KB32 * BLK16;
+    }
+    f32x4 bias4[PW], tp4[PW], tbias4[NQ], ttp4[NQ];
+    const int tq4 = 4 * ((lane >> 2) & 3);
+#pragma unroll
+    for (int c = 0; c < PW; ++c) {
+        const int col4 = gcol[c] * 16 + kq;
+        bias4[c] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
+        tp4[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
+                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int col4 = gcol[q] * 16 + tq4;
+        tbias4[q] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
+        ttp4[q] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
+                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int aoff[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) aoff[i] = ((rt0 + i) * 16 + rl) * lda + g * 32;
+    const int toff = (trow0 + (lane & 3)) * lda + g * 32;
+    f32x4 acc[NR][PW], tacc[NQ];
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+#pragma unroll
+        for (int c = 0; c < PW; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 bh[2][PW], bl[2][PW], ah[2][NR], al[2][NR], th[2], tl[2];
+#pragma unroll
+    for (int c = 0; c < PW; ++c) {
+        bh[0][c] = pre.h0[c];
+        bl[0][c] = pre.l0[c];
+        bh[1][c] = pre.h1[c];
+        bl[1][c] = pre.l1[c];
+    }
+    auto loadA = [&](int st, int kb) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            ah[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128);
+            al[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128 + 16);
+        }
+        th[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128);
+        tl[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128 + 16);
+    };
+    loadA(0, 0);
+    if constexpr (KB32 > 1) loadA(1, 1);
+#pragma unroll
+    for (int kb = 0; kb < KB32; ++kb) {
+        const int st = kb & 1;
+        // transposed tiles: weight fragment as the A operand (cf. GemmTile TRANS)
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[st][c], ah[st][i], acc[i][c], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], al[st][i], acc[i][c], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], ah[st][i], acc[i][c], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bl[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bl[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(tl[st]), tacc[q], 0, 0, 0);
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(tl[st]), tacc[q], 0, 0, 0);
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
+            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
+        }
+        if (kb + 2 < KB32) {
+#pragma unroll
+            for (int c = 0; c < PW; ++c) {
+                bh[st][c] = src.load(soff[c] + (kb + 2) * BLK16);
+                bl[st][c] = src.load(soff[c] + (kb + 2) * BLK16 + 1024);
+            }
+            loadA(st, kb + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    DPK_GEMM_HOOK(1);
+    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
+    constexpr float INV = 1.0f / W16_SCALE;
+    auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
+        if constexpr (MODE != E_CHEB1) return f32x4{0.f, 0.f, 0.f, 0.f};
+        if (e.tproj_pose_stride == 0) return uniform4;
+        const int pose = min(e.pose0 + row / J, e.pose_max);
+        return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
+    };
+    auto store = [&](int row, int col4, const f32x4& v) {
+        if constexpr (OUTSPLIT) split_store4(reinterpret_cast<char*>(e.dst + row * e.ldd), col4, v);
+        else *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
+    };
+    f32x4 old[NR][PW];
+    if constexpr (RES) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int c = 0; c < PW; ++c)
+                old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const int row = (rt0 + i) * 16 + rl;
+#pragma unroll
+        for (int c = 0; c < PW; ++c) {
+            const int col4 = gcol[c] * 16 + kq;
+            const f32x4 tp = tproj4(row, col4, tp4[c]);
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                v[r] = epi_value<MODE>(acc[i][c][r] * INV, bias4[c][r], tp[r], RES ? old[i][c][r] : 0.f);
+            store(row, col4, v);
+        }
+    }
+    const int row = trow0 + (lane & 3);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        f32x4 v = tacc[q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = sum4rows(v[r]);
+        if (g != 0 || (q == NQ - 1 && tail_dup) || row >= R) continue;
+        const int col4 = gcol[q] * 16 + tq4;
+        const f32x4 oldt = RES ? *reinterpret_cast<const f32x4*>(e.dst + row * e.ldd + col4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 tp = tproj4(row, col4, ttp4[q]);
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = epi_value<MODE>(v[r] * INV, tbias4[q][r], tp[r], oldt[r]);
+        store(row, col4, o);
+    }
+    DPK_GEMM_HOOK(2);
+}
+
+// Whole-workgroup split-fp16 GEMM: same wave roles as gemm_wg; the wave's NC/2 column tiles in
+// passes of PW16.  A: split rows (bytes, stride lda); B: this GEMM's split weight blocks.
+template <int NC, int KB32, int MODE, bool OUTSPLIT>
+__device__ __forceinline__ void gemm_wg16(const char* A, int lda, const char* Bp, int wave, int lane,
+                                          const EpiArgs& e, const BPre16<PW16>& pre) {
+    static_assert(NC % 2 == 0 && (NC / 2) % PW16 == 0 && (R == 68 || R == 34), "passes of 3 column tiles");
+    constexpr int NCW = NC / 2, NRW = R == 68 ? 2 : 1, NPASS = NCW / PW16;
+    const int pr = gemm_pr(wave);
+    const int rot = pr ? (PW16 + 1) / 2 : 0;
+    const bool dup = (PW16 & 1) && pr == 1;
+    const BSrc16 src = bsrc16<NC, KB32>(Bp, lane);
+    DPK_GEMM_HOOK(0);
+    gemm16_pass<NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, gemm_ch(wave) * NCW, rot, R - R % 16, dup,
+                                                     lane, e, pre);
+#pragma unroll 1
+    for (int ps = 1; ps < NPASS; ++ps) {
+        const int ctp = gemm_ch(wave) * NCW + ps * PW16;
+        BPre16<PW16> p2;
+#pragma unroll
+        for (int c = 0; c < PW16; ++c) {
+            const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
+            p2.h0[c] = src.load(b0);
+            p2.l0[c] = src.load(b0 + 1024);
+            p2.h1[c] = src.load(b0 + BLK16);
+            p2.l1[c] = src.load(b0 + BLK16 + 1024);
+        }
+        gemm16_pass<NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, ctp, rot, R - R % 16, dup, lane, e, p2);
+    }
+}
+
 // Output ChebConv (96->5, one col tile): waves 0-3, wave w = row tile w + tail row 64+w; the
 // raw accumulators go to a functor (DDIM update).
 template <int KB>
@@ -641,6 +927,7 @@ __device__ __forceinline__ float div_by(float x, float d, float r) {
 // part, part+3, ..., part+21 (interleaved, so the three lanes of a row hit different LDS
 // banks).  Two-pass fp32 statistics, pairwise sums combined in the same order in all three
 // lanes (bitwise identical mean/std per row).
+template <bool SPLIT = false>
 __device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
                                            int tid) {
     tid = opaque(tid);
@@ -682,7 +969,8 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
         f32x4 t;
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = div_by(gv[k] * dv[e][k], den, rcp) + sv[k];
-        *reinterpret_cast<f32x4*>(d + c0) = t;
+        if constexpr (SPLIT) split_store4(reinterpret_cast<char*>(d), c0, t);
+        else *reinterpret_cast<f32x4*>(d + c0) = t;
     }
 }
 
@@ -738,6 +1026,7 @@ __device__ __forceinline__ void pv16_keys(float& o, float pj_row, const float* v
     if constexpr (J + 1 < 16) pv16_keys<J + 1>(o, pj_row, vcol);
 }
 
+template <bool SPLIT = false>
 __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
     tid = opaque(tid);
     const int grp = tid >> 4, q = tid & 15;
@@ -798,7 +1087,10 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
     for (int d = 0; d < DK; ++d) o[d] = fmaf(pr[16], v16[d], o[d]);
 #pragma unroll
     for (int d = 0; d < DK; d += 4)
-        *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+        if constexpr (SPLIT)
+            split_store4(reinterpret_cast<char*>(out + (p * J + q) * LDX), h * DK + d, f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]});
+        else
+            *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
     // ---- query 16: lane j scores key j (its own key row); key 16 by every lane
     {
         float a16 = 0.f, b16 = 0.f;
@@ -824,12 +1116,17 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
         asm volatile("s_nop 1" ::: "memory");   // VALU write of pq -> DPP read (2 wait states)
         pv16_keys<0>(o0, pq, vcol + q);
         o0 = fmaf(pk, vcol[16 * LD2 + q], o0);
-        orows[16 * LDX + q] = o0;
+        char* row16 = reinterpret_cast<char*>(out + (p * J + 16) * LDX);
+        if constexpr (SPLIT) split_store1(row16, h * DK + q, o0);
+        else orows[16 * LDX + q] = o0;
         // all 16 lanes take part (the DPP broadcasts read every lane of the row); lanes q >= 8
         // read columns past the head (inside the row) and discard them
         pv16_keys<0>(o1, pq, vcol + q + 16);
         o1 = fmaf(pk, vcol[16 * LD2 + q + 16], o1);
-        if (q < DK - 16) orows[16 * LDX + q + 16] = o1;
+        if (q < DK - 16) {
+            if constexpr (SPLIT) split_store1(row16, h * DK + q + 16, o1);
+            else orows[16 * LDX + q + 16] = o1;
+        }
     }
 }
 
@@ -879,7 +1176,7 @@ static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 // K=288 GEMM reads one buffer; the packed weights follow the same order).
 // One thread per (pose, column pair).  SPARSE: compile-time pattern, packed values (scalar
 // loads); dense: 17x17 from the arena.  Sums run over increasing i in both (identical bits).
-template <bool SPARSE>
+template <bool SPARSE, bool SPLIT = false>
 __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int tid) {
     tid = opaque(tid);
     constexpr int G = 2, ng = D / G;
@@ -906,9 +1203,16 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
                 t2 = pfma(splat2(cw[J * J + j * J + i]), v[i], t2);
             }
         }
-        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
-        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
-        *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = v[j];
+        if constexpr (SPLIT) {
+            char* row = reinterpret_cast<char*>(b2 + (p * J + j) * LD2);
+            split_store2(row, c, t1);
+            split_store2(row, D + c, t2);
+            split_store2(row, 2 * D + c, v[j]);
+        } else {
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = v[j];
+        }
     }
 }
 
@@ -916,7 +1220,9 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
 // with uniform (scalar) loads.  One thread per (pose, column pair); in place.
 //   graph_apply:  buf[:, c] = L @ buf[:, c]
 //   graph_resid:  xs[:, c] += L @ y[:, c] + bias[c]   (fc2 reordered: L (X1 W2^T) + b2)
-template <bool RESID>
+// SPLIT_OUT (gemm mode 1, graph1): the product is fc1's A operand and is written split-fp16
+// into rows of stride LD2 (B2) instead of fp32 in place.
+template <bool RESID, bool SPLIT_OUT = false>
 __device__ __forceinline__ void graph_op(const float* __restrict__ L, const float* src, float* dst,
                                          const float* __restrict__ bias, int tid) {
     tid = opaque(tid);
@@ -934,6 +1240,10 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
         f32x2 acc = {0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < J; ++i) acc = pfma(splat2(L[j * J + i]), v[i], acc);
+        if constexpr (SPLIT_OUT) {
+            split_store2(reinterpret_cast<char*>(dst + (p * J + j) * LD2), c, acc);
+            continue;
+        }
         f32x2* o = reinterpret_cast<f32x2*>(dst + (p * J + j) * LDX + c);
         if (RESID) {
             *o = *o + (acc + bb);
@@ -979,12 +1289,14 @@ __device__ __forceinline__ void input_prep(const float* __restrict__ cw, const f
 // ---------------------------------------------------------------------------------------
 // The sampler: K DDIM steps (or one eps evaluation, or one GCNpose forward) for P poses
 // per workgroup.
-template <int MODE, bool SPARSE>
+template <int MODE, bool SPARSE, bool G16>
 // `arena` is a separate restrict kernel argument: the compiler can then prove the weight arena
 // is never written during the launch and turns its wave-uniform loads (Laplacians, Chebyshev
 // terms, LayerNorm gains, biases) into scalar s_load (in the SampleArgs struct it cannot, and
 // every such value became a vector load with its L2 latency exposed).
-__global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, const float* __restrict__ arena) {
+// G16: GEMMs on the split-fp16 path (gemm mode 1) with weights from `arena16`.
+__global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, const float* __restrict__ arena,
+                                                               const char* __restrict__ arena16) {
     constexpr bool EPS_MODE = MODE == M_EPS;
     constexpr bool POSE = MODE == M_POSE;
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
@@ -1061,30 +1373,55 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
 #pragma unroll 1
         for (int l = 0; l < NL; ++l) {
             const float* LW = W + l * LAYER_FLOATS;
+            const char* L16 = arena16 + (size_t)l * LAYER16_BYTES;
+            char* B1b = reinterpret_cast<char*>(B1);
+            char* B2b = reinterpret_cast<char*>(B2);
             // ---- x = x + MHA(LN0(x))   (GraAttenLayer, GraFormer.py:94-95)
             {
-                const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
-                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
-                BAR();
-                if (DPK_RUN(16 | 32)) {
-                    const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<18, 6, E_STORE>(B1, LDX, LW + OFF_QKV, wave, lane, e, pre);
+                const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
+                if constexpr (G16) {
+                    const auto pre = gemm16_prefetch<18, KB32_D>(L16 + O16_QKV, wave, lane);
+                    if (DPK_RUN(8)) layer_norm<true>(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 32)) gemm_wg16<18, KB32_D, E_STORE, false>(B1b, LDX * 4, L16 + O16_QKV, wave, lane, e, pre);
+                } else {
+                    const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
+                    if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 32)) gemm_wg<18, 6, E_STORE>(B1, LDX, LW + OFF_QKV, wave, lane, e, pre);
                 }
             }
             BAR();
             {
-                const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
-                if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
-                BAR();
-                if (DPK_RUN(16 | 64)) {
-                    const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 6, E_RESID>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
+                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
+                if constexpr (G16) {
+                    const auto pre = gemm16_prefetch<6, KB32_D>(L16 + O16_O, wave, lane);
+                    if (DPK_RUN(1)) attention<true>(B2, B1, a.mask, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 64)) gemm_wg16<6, KB32_D, E_RESID, false>(B1b, LDX * 4, L16 + O16_O, wave, lane, e, pre);
+                } else {
+                    const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
+                    if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
                 }
             }
             BAR();
             // ---- x = x + GraphNet(LN1(x)) = x + L (relu((L LN1(x)) W1^T + b1) W2^T) + b2
             //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
-            {
+            //      split path: graph1 writes fc1's A operand split into B2[:, 0:96]; fc1 writes
+            //      fc2's split A operand into B2[:, 96:288] (bytes 384..1152 of the row)
+            if constexpr (G16) {
+                const auto pre = gemm16_prefetch<12, KB32_D>(L16 + O16_FC1, wave, lane);
+                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
+                BAR();
+                if (DPK_RUN(2)) graph_op<false, true>(LW + OFF_LG, B1, B2, nullptr, tid);
+                BAR();
+                if (DPK_RUN(16 | 128)) {
+                    const EpiArgs e{B2 + D, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
+                    gemm_wg16<12, KB32_D, E_STORE_RELU, true>(B2b, LD2 * 4, L16 + O16_FC1, wave, lane, e, pre);
+                }
+            } else {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
                 BAR();
@@ -1096,35 +1433,55 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 }
             }
             {
-                const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
-                BAR();
-                if (DPK_RUN(16 | 256)) {
-                    const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 12, E_STORE_NB>(B2, LD2, LW + OFF_FC2, wave, lane, e, pre);
+                const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
+                if constexpr (G16) {
+                    const auto pre = gemm16_prefetch<6, KB32_D2>(L16 + O16_FC2, wave, lane);
+                    BAR();
+                    if (DPK_RUN(16 | 256))
+                        gemm_wg16<6, KB32_D2, E_STORE_NB, false>(B2b + D * 4, LD2 * 4, L16 + O16_FC2, wave, lane, e, pre);
+                } else {
+                    const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
+                    BAR();
+                    if (DPK_RUN(16 | 256)) gemm_wg<6, 12, E_STORE_NB>(B2, LD2, LW + OFF_FC2, wave, lane, e, pre);
                 }
             }
             {
-                const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
-                BAR();
-                if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
-                BAR();
-                // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
-                if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
-                BAR();
-                if (DPK_RUN(16 | 512)) {
-                    const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
-                    const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
-                    gemm_wg<6, 18, E_CHEB1>(B2, LD2, LW + OFF_C1, wave, lane, e, pre);
+                const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
+                const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
+                if constexpr (G16) {
+                    const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C1, wave, lane);
+                    BAR();
+                    if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
+                    BAR();
+                    // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, XS, B2, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 512)) gemm_wg16<6, KB32_D3, E_CHEB1, false>(B2b, LD2 * 4, L16 + O16_C1, wave, lane, e, pre);
+                } else {
+                    const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
+                    BAR();
+                    if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
+                    BAR();
+                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 512)) gemm_wg<6, 18, E_CHEB1>(B2, LD2, LW + OFF_C1, wave, lane, e, pre);
                 }
             }
             {
-                const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
-                BAR();
-                if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
-                BAR();
-                if (DPK_RUN(16 | 1024)) {
-                    const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<6, 18, E_RESID_RELU>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
+                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
+                if constexpr (G16) {
+                    const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C2, wave, lane);
+                    BAR();
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, B1, B2, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 1024))
+                        gemm_wg16<6, KB32_D3, E_RESID_RELU, false>(B2b, LD2 * 4, L16 + O16_C2, wave, lane, e, pre);
+                } else {
+                    const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
+                    BAR();
+                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
+                    BAR();
+                    if (DPK_RUN(16 | 1024)) gemm_wg<6, 18, E_RESID_RELU>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
                 }
             }
             BAR();
@@ -1272,6 +1629,9 @@ struct dpk_handle {
     float* tproj = nullptr;        // device: [cap][NL][D]
     int tproj_cap = 0;
     std::vector<float> h_arena;    // host staging of the arena
+    char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
+    std::vector<uint16_t> h_arena16;
+    int gemm_mode = 0;             // 0: fp32 MFMA, 1: 3x fp16-split MFMA (dpk_set_gemm_mode)
     std::vector<float> h_temb;
     bool have_graph = false, have_weights = false, have_sched = false;
     std::vector<float> h_coef;
@@ -1331,6 +1691,25 @@ static void pack_blocks(float* dst, int Kreal, int Nreal, int KB, int NC, F w) {
                 }
 }
 
+// Split W_eff * W16_SCALE into fp16 hi + lo 16x16x32 B fragments [NC][KB32][hi|lo][64][8].
+// hi = fp16(v) (RNE), lo = fp16(v - hi); v - hi is exact in fp32 (Sterbenz).
+template <class F>
+static void pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
+    for (int ct = 0; ct < NC; ++ct)
+        for (int kb = 0; kb < KB32; ++kb)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int i = 0; i < 8; ++i) {
+                    const int k = kb * 32 + 8 * (lane >> 4) + i;
+                    const int n = ct * 16 + (lane & 15);
+                    const float v = (k < Kreal && n < Nreal) ? w(k, n) * W16_SCALE : 0.f;
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    const size_t base = ((size_t)(ct * KB32 + kb) * BLK16) / 2;
+                    dst[base + lane * 8 + i] = __builtin_bit_cast(uint16_t, hi);
+                    dst[base + 512 + lane * 8 + i] = __builtin_bit_cast(uint16_t, lo);
+                }
+}
+
 // Row of a ChebConv weight (3,1,96,out) viewed as [3*96][out] that multiplies column k of
 // cheb_prep's [T1X | T2X | X] buffer.
 static inline int cheb_row(int k) { return ((k / D + 1) % 3) * D + k % D; }
@@ -1380,10 +1759,25 @@ static int ensure_tproj(dpk_handle* h, int slots) {
 static int upload(dpk_handle* h) {
     HIPCHK(h, hipSetDevice(h->device));
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
+    if (!h->arena16) HIPCHK(h, hipMalloc(&h->arena16, (size_t)ARENA16_BYTES));
+    HIPCHK(h, hipMemcpy(h->arena16, h->h_arena16.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
     if (!h->temb) HIPCHK(h, hipMalloc(&h->temb, (size_t)TEMB_FLOATS * 4));
     HIPCHK(h, hipMemcpy(h->arena, h->h_arena.data(), (size_t)ARENA_FLOATS * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->temb, h->h_temb.data(), (size_t)TEMB_FLOATS * 4, hipMemcpyHostToDevice));
     return DPK_OK;
+}
+
+// the sampler kernel for the handle's graph pattern and GEMM mode
+template <int MODE>
+static void launch_sampler(dpk_handle* h, dim3 grid, hipStream_t st, const SampleArgs& a) {
+    const bool g16 = h->gemm_mode == 1;
+    if (h->sparse_graph) {
+        if (g16) hipLaunchKernelGGL((sample_kernel<MODE, true, true>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+        else hipLaunchKernelGGL((sample_kernel<MODE, true, false>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+    } else {
+        if (g16) hipLaunchKernelGGL((sample_kernel<MODE, false, true>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+        else hipLaunchKernelGGL((sample_kernel<MODE, false, false>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+    }
 }
 
 extern "C" {
@@ -1414,6 +1808,7 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (const char* pd = getenv("DPK_PHASE_DELAY")) h->phase_delay = atoi(pd);
     else h->phase_delay = WG_PER_CU == 2 ? 60000 : 0;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
+    h->h_arena16.assign(ARENA16_BYTES / 2, 0);
     h->h_temb.assign(TEMB_FLOATS, 0.f);
     *out = h;
     return DPK_OK;
@@ -1423,6 +1818,7 @@ void dpk_destroy(dpk_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->arena) (void)hipFree(h->arena);
+    if (h->arena16) (void)hipFree(h->arena16);
     if (h->temb) (void)hipFree(h->temb);
     if (h->coef) (void)hipFree(h->coef);
     if (h->tproj) (void)hipFree(h->tproj);
@@ -1548,6 +1944,16 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         // ChebConv weight (3,1,in,out), rows in cheb_prep's B2 order [T1X | T2X | X]: k -> order (k/96+1)%3
         pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
         pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
+        uint16_t* L16 = h->h_arena16.data() + (size_t)l * LAYER16_BYTES / 2;
+        pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
+            const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
+            return w[(n % D) * D + k];
+        });
+        pack16(L16 + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; });
+        pack16(L16 + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
+        pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
+        pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
+        pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
         for (int c = 0; c < D; ++c) {
             Lw[OFF_BQKV + c] = bq[c];
             Lw[OFF_BQKV + D + c] = bk[c];
@@ -1685,10 +2091,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     a.mask = h->mask;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
-    if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_EPS, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
-    else
-        hipLaunchKernelGGL((sample_kernel<M_EPS, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
+    launch_sampler<M_EPS>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -1738,10 +2141,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
 #endif
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
-    else
-        hipLaunchKernelGGL((sample_kernel<M_SAMPLE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
+    launch_sampler<M_SAMPLE>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return DPK_OK;
@@ -1770,12 +2170,16 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     a.mask = h->mask;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
-    if (h->sparse_graph)
-        hipLaunchKernelGGL((sample_kernel<M_POSE, true>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
-    else
-        hipLaunchKernelGGL((sample_kernel<M_POSE, false>), dim3((N + P - 1) / P), dim3(NT), 0, st, a, h->arena);
+    launch_sampler<M_POSE>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
     if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
+    return DPK_OK;
+}
+
+int dpk_set_gemm_mode(dpk_handle* h, int mode) {
+    if (!h) return DPK_E_INVALID;
+    if (mode != 0 && mode != 1) return fail(h, DPK_E_INVALID, "dpk_set_gemm_mode: mode must be 0 (fp32) or 1 (3xfp16)");
+    h->gemm_mode = mode;
     return DPK_OK;
 }
 

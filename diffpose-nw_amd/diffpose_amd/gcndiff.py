@@ -147,6 +147,17 @@ class _HipModel:
             raise ValueError(f"x on {x.device}, model on {self.device}")
         return x.contiguous()
 
+    GEMM_MODES = {"fp32": 0, "f16x3": 1}
+
+    def set_gemm_mode(self, mode: str = "fp32") -> None:
+        """Arithmetic of the per-layer GEMMs (see dpk_set_gemm_mode): "fp32" (default, fp32 MFMA)
+        or "f16x3" (3-term fp16-split MFMA, fp32 accumulate).  Not a reference option: the
+        reference runs fp32 throughout, and "fp32" is what its parity is pinned on."""
+        if mode not in self.GEMM_MODES:
+            raise ValueError(f"gemm mode must be one of {sorted(self.GEMM_MODES)}, got {mode!r}")
+        _lib.check(self._h, "dpk_set_gemm_mode", _lib.lib().dpk_set_gemm_mode(self._h, self.GEMM_MODES[mode]))
+        self.gemm_mode = mode
+
     def profile(self, enable: bool = True) -> None:
         """Bracket each model-kernel launch with HIP events (see dpk_profile)."""
         _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))

@@ -128,6 +128,15 @@ int dpk_pose(dpk_handle* h, const float* x2d_dev, float* xyz_dev, float* uvxyz_d
 int dpk_pose_metrics(const float* out_uvxyz_dev, const float* targets_dev, int F, int H, int root_mode,
                      double* p1_dev, double* p2_dev, float* xyz_dev, void* stream);
 
+/* GEMM arithmetic of the sampler's transformer/ResChebGC GEMMs (not part of the reference
+ * interface; the reference computes everything in fp32 on its device):
+ *   mode 0 (default): fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 accumulate;
+ *   mode 1: 3-term fp16 split (a = a_hi + a_lo, w*64 = w_hi + w_lo; a_hi w_hi + a_hi w_lo +
+ *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products.
+ * The input/output ChebConvs, LayerNorm, attention and the DDIM update stay fp32 in both.
+ * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle. */
+int dpk_set_gemm_mode(dpk_handle* h, int mode);
+
 /* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /
  * dpk_eps brackets its sampler-kernel launch with a pair of HIP events on the
  * caller's stream.  dpk_profile_read waits for the recorded events and returns up to
