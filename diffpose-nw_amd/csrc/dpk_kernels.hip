@@ -922,72 +922,7 @@ __device__ __forceinline__ float div_by(float x, float d, float r) {
     return fmaf(e, r, q);
 }
 
-// LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b, one pass:
-// 3 lanes per row, 21 rows per wave.  Lane `part` of a row owns the 16-byte chunks
-// part, part+3, ..., part+21 (interleaved, so the three lanes of a row hit different LDS
-// banks).  Two-pass fp32 statistics, pairwise sums combined in the same order in all three
-// lanes (bitwise identical mean/std per row).
-template <bool SPLIT = false>
-__device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
-                                           int tid) {
-    tid = opaque(tid);
-    const int w = tid >> 6, lane = tid & 63;
-    const int row = w * 21 + lane / 3, part = lane % 3;
-    const bool ok = lane < 63 && row < R;
-    const int rr = ok ? row : R - 1;
-    const float* s = src + rr * LDX;
-    f32x4 v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = *reinterpret_cast<const f32x4*>(s + 4 * (part + 3 * e));
-    auto psum = [](const f32x4 (&x)[8]) {
-        f32x4 a = (x[0] + x[1]) + (x[2] + x[3]);
-        f32x4 b = (x[4] + x[5]) + (x[6] + x[7]);
-        const f32x4 c = a + b;
-        return (c[0] + c[1]) + (c[2] + c[3]);
-    };
-    const int base = (lane / 3) * 3;
-    const float ls = psum(v);
-    const float s0 = __shfl(ls, base, 64), s1 = __shfl(ls, base + 1, 64), s2 = __shfl(ls, base + 2, 64);
-    const float mean = ((s0 + s1) + s2) / (float)D;
-    f32x4 dv[8], sq[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        dv[e] = v[e] - mean;
-        sq[e] = dv[e] * dv[e];
-    }
-    const float lq = psum(sq);
-    const float q0 = __shfl(lq, base, 64), q1 = __shfl(lq, base + 1, 64), q2 = __shfl(lq, base + 2, 64);
-    const float den = sqrtf(((q0 + q1) + q2) / (float)(D - 1)) + LN_EPS;
-    const float rcp = 1.0f / den;
-    if (!ok) return;
-    float* d = dst + row * LDX;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int c0 = 4 * (part + 3 * e);
-        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c0);
-        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c0);
-        f32x4 t;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = div_by(gv[k] * dv[e][k], den, rcp) + sv[k];
-        if constexpr (SPLIT) split_store4(reinterpret_cast<char*>(d), c0, t);
-        else *reinterpret_cast<f32x4*>(d + c0) = t;
-    }
-}
-
-// 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
-// projections).  One DPP row (16 lanes) per (pose, head); lane q owns query q AND key/value
-// row q in registers.  Keys/values 0..15 reach the other lanes of the row by DPP row_newbcast
-// fused into the FMA (v_fmac_f32_dpp), so the K/V rows are read from LDS once per lane instead
-// of once per (query, key).  Row 16 (key/value 16) is read by every lane of the row; query 16
-// is computed cooperatively (lane j scores key j; lane q sums value column q over the keys).
-template <int J>
-__device__ __forceinline__ void fmac_bcast(float& acc, float row_src, float x) {
-    // acc += row_src[lane J of this 16-lane row] * x
-    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-        : "+v"(acc)
-        : "v"(row_src), "v"(x), "i"(J));
-}
-
+// DPP row (16-lane) rotations and all-reduces
 template <int J>
 __device__ __forceinline__ float row_ror(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
@@ -1005,6 +940,114 @@ __device__ __forceinline__ float row_sum(float v) {
     v += row_ror<4>(v);
     v += row_ror<2>(v);
     return v + row_ror<1>(v);
+}
+
+// LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b.
+// Rows 0..63: a DPP quad (4 lanes) per row, 16 rows per wave; lane `part` of a row owns the
+// 16-byte chunks part, part+4, ..., part+20 (interleaved across LDS banks).  Rows 64..67: wave w
+// takes row 64+w, 16 lanes x 6 elements (columns 2*lane + 32*e), lanes 16..63 mirror 0..15.
+// Two-pass fp32 statistics; the cross-lane sums are DPP all-reduces whose operands pair up
+// commutatively, so every lane of a row holds bitwise the same mean/std.  Divisions by 96 and
+// 95 and by the row's std use div_by (correctly rounded, as the reference's true division).
+__device__ __forceinline__ float quad_sum(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                               0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                                     0x4E, 0xf, 0xf, false));   // [2,3,0,1]
+}
+__device__ __forceinline__ f32x4 div_by4(f32x4 x, float d, float r) {
+    const f32x4 q = x * r;
+    const f32x4 e = __builtin_elementwise_fma(-q, f32x4{d, d, d, d}, x);
+    return __builtin_elementwise_fma(e, f32x4{r, r, r, r}, q);
+}
+__device__ __forceinline__ f32x2 div_by2(f32x2 x, float d, float r) {
+    const f32x2 q = x * r;
+    const f32x2 e = __builtin_elementwise_fma(-q, f32x2{d, d}, x);
+    return __builtin_elementwise_fma(e, f32x2{r, r}, q);
+}
+template <bool SPLIT = false>
+__device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
+                                           int tid) {
+    tid = opaque(tid);
+    const int w = tid >> 6, lane = tid & 63;
+    constexpr float RD = 1.0f / (float)D, RD1 = 1.0f / (float)(D - 1);
+    // ---- rows 0..63 (0..31 at P=2: waves 2-3 compute row 31 and store nothing)
+    constexpr int RM = R - R % 16, RT = R % 16;
+    static_assert(RT <= 4, "tail rows: one per wave");
+    const bool main_ok = w * 16 < RM, tail_ok = w < RT;
+    const int row = main_ok ? w * 16 + (lane >> 2) : RM - 1, part = lane & 3;
+    const float* s = src + row * LDX;
+    f32x4 v[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) v[e] = *reinterpret_cast<const f32x4*>(s + 4 * (part + 4 * e));
+    // ---- row 64 + w
+    const int tl = lane & 15;
+    const float* st = src + (RM + (tail_ok ? w : 0)) * LDX;
+    f32x2 u[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) u[e] = *reinterpret_cast<const f32x2*>(st + 2 * tl + 32 * e);
+    auto psum6 = [](const f32x4 (&x)[6]) {
+        const f32x4 c = ((x[0] + x[1]) + (x[2] + x[3])) + (x[4] + x[5]);
+        return (c[0] + c[1]) + (c[2] + c[3]);
+    };
+    auto psum3 = [](const f32x2 (&x)[3]) {
+        const f32x2 c = (x[0] + x[1]) + x[2];
+        return c[0] + c[1];
+    };
+    const float mean = div_by(quad_sum(psum6(v)), (float)D, RD);
+    const float tmean = div_by(row_sum(psum3(u)), (float)D, RD);
+    f32x4 dv[6], sq[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        dv[e] = v[e] - mean;
+        sq[e] = dv[e] * dv[e];
+    }
+    f32x2 du[3], squ[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        du[e] = u[e] - tmean;
+        squ[e] = du[e] * du[e];
+    }
+    const float den = sqrtf(div_by(quad_sum(psum6(sq)), (float)(D - 1), RD1)) + LN_EPS;
+    const float tden = sqrtf(div_by(row_sum(psum3(squ)), (float)(D - 1), RD1)) + LN_EPS;
+    const float rcp = 1.0f / den, trcp = 1.0f / tden;
+    float* d = dst + row * LDX;
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        if (!main_ok) break;
+        const int c0 = 4 * (part + 4 * e);
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c0);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c0);
+        const f32x4 t = div_by4(gv * dv[e], den, rcp) + sv;
+        if constexpr (SPLIT) split_store4(reinterpret_cast<char*>(d), c0, t);
+        else *reinterpret_cast<f32x4*>(d + c0) = t;
+    }
+    if (lane < 16 && tail_ok) {
+        float* dt = dst + (RM + w) * LDX;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            const int c0 = 2 * tl + 32 * e;
+            const f32x2 gv = *reinterpret_cast<const f32x2*>(gain + c0);
+            const f32x2 sv = *reinterpret_cast<const f32x2*>(shift + c0);
+            const f32x2 t = div_by2(gv * du[e], tden, trcp) + sv;
+            if constexpr (SPLIT) split_store2(reinterpret_cast<char*>(dt), c0, t);
+            else *reinterpret_cast<f32x2*>(dt + c0) = t;
+        }
+    }
+}
+
+// 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
+// projections).  One DPP row (16 lanes) per (pose, head); lane q owns query q AND key/value
+// row q in registers.  Keys/values 0..15 reach the other lanes of the row by DPP row_newbcast
+// fused into the FMA (v_fmac_f32_dpp), so the K/V rows are read from LDS once per lane instead
+// of once per (query, key).  Row 16 (key/value 16) is read by every lane of the row; query 16
+// is computed cooperatively (lane j scores key j; lane q sums value column q over the keys).
+template <int J>
+__device__ __forceinline__ void fmac_bcast(float& acc, float row_src, float x) {
+    // acc += row_src[lane J of this 16-lane row] * x
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc)
+        : "v"(row_src), "v"(x), "i"(J));
 }
 
 // one feature d of this lane's query against keys 0..15 (key rows broadcast from their owner
@@ -1632,6 +1675,7 @@ struct dpk_handle {
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
     int gemm_mode = 0;             // 0: fp32 MFMA, 1: 3x fp16-split MFMA (dpk_set_gemm_mode)
+    bool w16_ok = true;            // loaded weights fit the split-fp16 packing (|w| < 1015)
     std::vector<float> h_temb;
     bool have_graph = false, have_weights = false, have_sched = false;
     std::vector<float> h_coef;
@@ -1694,7 +1738,8 @@ static void pack_blocks(float* dst, int Kreal, int Nreal, int KB, int NC, F w) {
 // Split W_eff * W16_SCALE into fp16 hi + lo 16x16x32 B fragments [NC][KB32][hi|lo][64][8].
 // hi = fp16(v) (RNE), lo = fp16(v - hi); v - hi is exact in fp32 (Sterbenz).
 template <class F>
-static void pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
+static float pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
+    float wmax = 0.f;
     for (int ct = 0; ct < NC; ++ct)
         for (int kb = 0; kb < KB32; ++kb)
             for (int lane = 0; lane < 64; ++lane)
@@ -1702,12 +1747,14 @@ static void pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
                     const int k = kb * 32 + 8 * (lane >> 4) + i;
                     const int n = ct * 16 + (lane & 15);
                     const float v = (k < Kreal && n < Nreal) ? w(k, n) * W16_SCALE : 0.f;
+                    wmax = fmaxf(wmax, fabsf(v));
                     const _Float16 hi = (_Float16)v;
                     const _Float16 lo = (_Float16)(v - (float)hi);
                     const size_t base = ((size_t)(ct * KB32 + kb) * BLK16) / 2;
                     dst[base + lane * 8 + i] = __builtin_bit_cast(uint16_t, hi);
                     dst[base + 512 + lane * 8 + i] = __builtin_bit_cast(uint16_t, lo);
                 }
+    return wmax;
 }
 
 // Row of a ChebConv weight (3,1,96,out) viewed as [3*96][out] that multiplies column k of
@@ -1900,6 +1947,7 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
     const bool pose = h->kind == 1;
     const int cin = pose ? CIN_POSE : CIN, cout = pose ? COUT_POSE : COUT;
     float* A = h->h_arena.data();
+    float w16max = 0.f;             // largest |64 w| of the split-fp16 GEMM weights
     for (int l = 0; l < NL; ++l) {
         float* Lw = A + (size_t)l * LAYER_FLOATS;
         const std::string at = "atten_layers." + std::to_string(l) + ".";
@@ -1945,15 +1993,15 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
         pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
         uint16_t* L16 = h->h_arena16.data() + (size_t)l * LAYER16_BYTES / 2;
-        pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
+        w16max = fmaxf(w16max, pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
             const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
             return w[(n % D) * D + k];
-        });
-        pack16(L16 + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; });
-        pack16(L16 + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
-        pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
-        pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
-        pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
+        }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; }));
         for (int c = 0; c < D; ++c) {
             Lw[OFF_BQKV + c] = bq[c];
             Lw[OFF_BQKV + D + c] = bk[c];
@@ -1978,6 +2026,8 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
             }
         }
     }
+    // fp16 hi parts must stay finite: |64 w| below the largest fp16 (65504), with margin
+    h->w16_ok = w16max < 65000.f;
     GET(wi, "gconv_input.weight", 3 * cin * D);
     GET(bi, "gconv_input.bias", D);
     GET(wout, "gconv_output.weight", 3 * D * cout);
@@ -2065,6 +2115,9 @@ static int check_ready(dpk_handle* h, int kind = 0) {
                                          : "GCNpose handle (coords 2->3): use dpk_pose");
     if (!h->have_graph) return fail(h, DPK_E_STATE, "graph (adjacency) not set");
     if (!h->have_weights) return fail(h, DPK_E_STATE, "weights not loaded");
+    if (h->gemm_mode == 1 && !h->w16_ok)
+        return fail(h, DPK_E_UNSUPPORTED, "gemm mode 1 (3x fp16): a GEMM weight has |w| >= 1015, outside the split-fp16 "
+                                          "packing range; use gemm mode 0 (fp32)");
     return DPK_OK;
 }
 

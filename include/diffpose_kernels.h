@@ -134,7 +134,10 @@ int dpk_pose_metrics(const float* out_uvxyz_dev, const float* targets_dev, int F
  *   mode 1: 3-term fp16 split (a = a_hi + a_lo, w*64 = w_hi + w_lo; a_hi w_hi + a_hi w_lo +
  *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products.
  * The input/output ChebConvs, LayerNorm, attention and the DDIM update stay fp32 in both.
- * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle. */
+ * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle.  Range: mode 1 needs
+ * every GEMM weight |w| < 1015 (else those calls return DPK_E_UNSUPPORTED) and GEMM inputs
+ * (LayerNorm/attention/graph/Chebyshev outputs) below 65504 in magnitude; an overflow there
+ * shows as non-finite outputs. */
 int dpk_set_gemm_mode(dpk_handle* h, int mode);
 
 /* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /

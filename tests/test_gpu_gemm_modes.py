@@ -154,3 +154,25 @@ def test_gcnpose_f16x3_vs_golden(golden):
 def test_bad_gemm_mode_raises(model):
     with pytest.raises(ValueError):
         model.set_gemm_mode("bf16")
+
+
+def test_out_of_range_weights_are_refused():
+    """Weights outside the fp16 split range make f16x3 calls fail loudly; fp32 still runs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from diffpose_amd._lib import DpkError
+
+    sd = synthetic_state_dict()
+    sd["atten_layers.2.self_attn.linears.1.weight"] = sd["atten_layers.2.self_attn.linears.1.weight"].copy()
+    sd["atten_layers.2.self_attn.linears.1.weight"][3, 5] = 2000.0
+    m = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+    m.load_state_dict(sd)
+    x, _ = synthetic_batch(4, seed=1)
+    xd = torch.from_numpy(x).cuda()
+    t = torch.full((4,), 10.0, device="cuda:0")
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device="cuda:0")
+    m(xd, mask, t, 0)
+    m.set_gemm_mode("f16x3")
+    with pytest.raises(DpkError, match="UNSUPPORTED|split-fp16"):
+        m(xd, mask, t, 0)
+    m.close()

@@ -21,10 +21,15 @@ SO = os.path.join(ROOT, "build", "trace", "libdpk_trace.so")
 
 # stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
 # ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
-def _events():
+# the split-fp16 GEMMs (gemm mode f16x3) run a wave's column tiles in passes of 3 and stamp per pass
+def _events(gemm_mode="fp32"):
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
-    gemm = lambda n: ev.extend([(n, "loop"), (n, "epi")])
+    npass = {"QKV": 3, "fc1": 2} if gemm_mode == "f16x3" else {}
+
+    def gemm(n):
+        for _ in range(npass.get(n.split(".")[-1], 1)):
+            ev.extend([(n, "loop"), (n, "epi")])
     bar("input_prep"); gemm("input_gemm"); bar("input_gemm")
     for l in range(5):
         p = f"L{l}."
@@ -38,9 +43,6 @@ def _events():
     return ev
 
 
-EVENTS = _events()
-
-
 def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     src = [os.path.join(ROOT, "diffpose-nw_amd", "csrc", f) for f in ("dpk_kernels.hip", "dpk_metrics.hip")]
@@ -51,7 +53,8 @@ def build():
     print("built", SO)
 
 
-def run(step=10, frames=1024):
+def run(step=10, frames=1024, gemm_mode="fp32"):
+    EVENTS = _events(gemm_mode)
     os.environ["DPK_LIB"] = SO
     sys.path.insert(0, os.path.join(ROOT, "diffpose-nw_amd"))
     import numpy as np
@@ -67,6 +70,7 @@ def run(step=10, frames=1024):
     L.dpk_debug_trace.restype = ctypes.c_int
     m = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
     m.load_state_dict(synthetic_state_dict())
+    m.set_gemm_mode(gemm_mode)
     x = torch.from_numpy(synthetic_batch(frames)[0]).cuda()
     seq = make_seq("uniform", 50, 50)
     b = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3, num_diffusion_timesteps=51)).float()
@@ -92,6 +96,8 @@ def run(step=10, frames=1024):
         name, kind = EVENTS[k + 1]
         key = name.split(".", 1)[1] if name.startswith("L") and "." in name else name
         part = {"pre": "compute", "post": "wait", "loop": "loop", "epi": "epilogue"}[kind]
+        if kind == "loop" and EVENTS[k][1] == "epi":
+            part = "loop"                       # next pass of the same GEMM
         if kind == "pre" and EVENTS[k][1] == "epi":
             part = "after_epi"
         a = agg.setdefault(key, {})
@@ -112,8 +118,9 @@ if __name__ == "__main__":
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--step", type=int, default=10)
+    ap.add_argument("--gemm", choices=("fp32", "f16x3"), default="fp32")
     a = ap.parse_args()
     if a.build:
         build()
     if a.run:
-        run(a.step)
+        run(a.step, gemm_mode=a.gemm)
