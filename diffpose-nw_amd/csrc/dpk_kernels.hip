@@ -125,7 +125,8 @@ constexpr int OFF_LN0B = OFF_LN0A + D;
 constexpr int OFF_LN1A = OFF_LN0B + D;
 constexpr int OFF_LN1B = OFF_LN1A + D;
 constexpr int OFF_LG = OFF_LN1B + D;                        // 17x17
-constexpr int LAYER_FLOATS = ((OFF_LG + J * J + 63) / 64) * 64;
+constexpr int OFF_LGF = ((OFF_LG + J * J + 63) / 64) * 64;  // graph_mma operands: [5 k][64 lanes] L^T, then row 16
+constexpr int LAYER_FLOATS = OFF_LGF + 2 * 5 * 64;
 constexpr int OFF_WIN = NL * LAYER_FLOATS;                  // [6 ct][1 kb]  (K=15 padded to 16)
 constexpr int OFF_WOUT = OFF_WIN + 6 * 1 * BLK;             // [1 ct][18 kb] (N=5 padded to 16)
 constexpr int OFF_BIN = OFF_WOUT + 1 * KB_D3 * BLK;
@@ -279,6 +280,17 @@ __device__ __forceinline__ float sum4rows(float v) {
     float c = s1, d = s1;
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
     return c + d;
+}
+
+// Reduce-scatter of 4 registers over the 4 lane rows: lane l returns the sum over rows of
+// register (l>>4) at row position l&15, summed ((row0 + row2) + (row1 + row3)) like sum4rows.
+// 3 permlane swaps for 4 values instead of sum4rows' 8 (tools/rs4_probe.hip checks the map).
+__device__ __forceinline__ float rs4rows(float v0, float v1, float v2, float v3) {
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v0), "+v"(v2));
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v1), "+v"(v3));
+    float a = v0 + v2, b = v1 + v3;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return a + b;
 }
 
 // Launder a value through an empty asm so LLVM cannot hoist per-thread address math out
@@ -515,17 +527,18 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         tp4[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    // tail tiles (TM_MFMA4): lane l holds tail row l&3, columns 4*((l>>2)&3)..+3
-    const int tq4 = 4 * ((lane >> 2) & 3);
-    f32x4 tbias4[NQ], ttp4[NQ];
+    // tail tiles (TM_MFMA4): after the k-slice reduce-scatter lane l holds tail row l&3,
+    // column tcol of the tile
+    const int tcol = 4 * ((lane >> 2) & 3) + (lane >> 4);
+    float tbias[NQ], ttp[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        tbias4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ttp4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        tbias[q] = 0.f;
+        ttp[q] = 0.f;
         if constexpr (TM == TM_MFMA4) {
-            const int col4 = gcol[q] * 16 + tq4;
-            if (MODE != E_STORE_NB) tbias4[q] = *reinterpret_cast<const f32x4*>(e.bias + col4);
-            if (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ttp4[q] = *reinterpret_cast<const f32x4*>(e.tproj + col4);
+            const int col = gcol[q] * 16 + tcol;
+            if (MODE != E_STORE_NB) tbias[q] = e.bias[col];
+            if (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ttp[q] = e.tproj[col];
         }
     }
     const BSrc src = bsrc<NC, KB>(Bp, ct0, lane);
@@ -591,26 +604,20 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
             *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
         }
     }
-    const int grp = lane >> 4;
     if constexpr (TM == TM_VALU) {
         static_assert(TM != TM_VALU, "gemm_wave computes transposed tiles; VALU tails are gemm_out's");
     } else if constexpr (TM == TM_MFMA4) {
-        // reduce the 4 k-slices; lanes 0..15 then hold tail row l&3, columns tq4..tq4+3 of tile q
+        // reduce-scatter the 4 k-slices: lane l then holds tail row l&3, column tcol of tile q
         const int row = trow0 + (lane & 3);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            f32x4 v = g.tacc[q];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = sum4rows(v[r]);
-            if (grp != 0 || (q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
-            const int col4 = gcol[q] * 16 + tq4;
-            f32x4* dp = reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4);
-            const f32x4 oldt = RES ? *dp : f32x4{0.f, 0.f, 0.f, 0.f};
-            const f32x4 tp = tproj4(row, col4, ttp4[q]);
-            f32x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = epi_value<MODE>(v[r], tbias4[q][r], tp[r], oldt[r]);
-            *dp = o;
+            const float v = rs4rows(g.tacc[q][0], g.tacc[q][1], g.tacc[q][2], g.tacc[q][3]);
+            if ((q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
+            const int col = gcol[q] * 16 + tcol;
+            float* dp = e.dst + row * e.ldd + col;
+            const float oldt = RES ? *dp : 0.f;
+            const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
+            *dp = epi_value<MODE>(v, tbias[q], tp, oldt);
         }
     }
     DPK_GEMM_HOOK(2);
@@ -703,8 +710,9 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
         gcol[c] = pass_col<PW>(ctp, c, rot);
         soff[c] = gcol[c] * KB32 * BLK16;
     }
-    f32x4 bias4[PW], tp4[PW], tbias4[NQ], ttp4[NQ];
-    const int tq4 = 4 * ((lane >> 2) & 3);
+    f32x4 bias4[PW], tp4[PW];
+    float tbias[NQ], ttp[NQ];
+    const int tcol = 4 * ((lane >> 2) & 3) + g;     // tail column of this lane after the reduce-scatter
 #pragma unroll
     for (int c = 0; c < PW; ++c) {
         const int col4 = gcol[c] * 16 + kq;
@@ -714,10 +722,9 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const int col4 = gcol[q] * 16 + tq4;
-        tbias4[q] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
-        ttp4[q] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
-                                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int col = gcol[q] * 16 + tcol;
+        tbias[q] = MODE == E_STORE_NB ? 0.f : e.bias[col];
+        ttp[q] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
     }
     int aoff[NR];
 #pragma unroll
@@ -822,17 +829,14 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
     const int row = trow0 + (lane & 3);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        f32x4 v = tacc[q];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = sum4rows(v[r]);
-        if (g != 0 || (q == NQ - 1 && tail_dup) || row >= R) continue;
-        const int col4 = gcol[q] * 16 + tq4;
-        const f32x4 oldt = RES ? *reinterpret_cast<const f32x4*>(e.dst + row * e.ldd + col4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 tp = tproj4(row, col4, ttp4[q]);
-        f32x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = epi_value<MODE>(v[r] * INV, tbias4[q][r], tp[r], oldt[r]);
-        store(row, col4, o);
+        const float v = rs4rows(tacc[q][0], tacc[q][1], tacc[q][2], tacc[q][3]);
+        if ((q == NQ - 1 && tail_dup) || row >= R) continue;
+        const int col = gcol[q] * 16 + tcol;
+        const float oldt = RES ? e.dst[row * e.ldd + col] : 0.f;
+        const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
+        const float o = epi_value<MODE>(v * INV, tbias[q], tp, oldt);
+        if constexpr (OUTSPLIT) split_store1(reinterpret_cast<char*>(e.dst + row * e.ldd), col, o);
+        else e.dst[row * e.ldd + col] = o;
     }
     DPK_GEMM_HOOK(2);
 }
@@ -1217,16 +1221,19 @@ static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 
 // Chebyshev prologue: B2 = [T1 src | T2 src | src] (ChebConv.py:83, term order rotated so the
 // K=288 GEMM reads one buffer; the packed weights follow the same order).
-// One thread per (pose, column pair).  SPARSE: compile-time pattern, packed values (scalar
-// loads); dense: 17x17 from the arena.  Sums run over increasing i in both (identical bits).
+// Wave w = pose w, lane = column pair (lanes 48..63 idle), so a wave reads only rows its own
+// earlier LDS writes produced when it follows graph_mma (no workgroup barrier in between).
+// SPARSE: compile-time pattern, packed values (scalar loads); dense: 17x17 from the arena.
+// Sums run over increasing i in both (identical bits).
 template <bool SPARSE, bool SPLIT = false>
-__device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int tid) {
-    tid = opaque(tid);
+__device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int wave,
+                                          int lane) {
+    lane = opaque(lane);
     constexpr int G = 2, ng = D / G;
-    static_assert(P * ng <= NT, "one item per thread");
-    if (tid >= P * ng) return;
-    const int p = tid / ng;
-    const int c = (tid - p * ng) * G;
+    static_assert(ng <= 64 && P <= NW, "one pose per wave, one column pair per lane");
+    if (wave >= P || lane >= ng) return;
+    const int p = wave;
+    const int c = lane * G;
     f32x2 v[J];
 #pragma unroll
     for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
@@ -1292,6 +1299,89 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
             *o = *o + (acc + bb);
         } else {
             *o = acc;
+        }
+    }
+}
+
+// GraphNet product on the matrix cores: wave w = pose w computes out^T = X^T L^T for its 17
+// rows with v_mfma_f32_16x16x4_f32 (M = 96 columns in 6 tiles, N = joints 0..15, K = joints in
+// 5 steps of 4, rows past 16 clamped and multiplied by zero), so lane l ends with out[j = l&15]
+// [c .. c+3] (16-byte stores).  Joint 16 (the 17th output row) from the same A fragments:
+// per-lane partial sums over the lane's k-slice, summed over the 4 lane groups by permlane.
+// LF: the layer's fragments (OFF_LGF): [s][lane] = L[lane&15][4s + (lane>>4)] and
+// [5 + s][lane] = L[16][4s + (lane>>4)] (0 past joint 16).
+//   RESID:     dst (stride LDX) += out + bias          (graph2: x + L (Y W2^T) + b2)
+//   SPLIT_OUT: out written split-fp16 into rows of stride LD2 (gemm mode 1, graph1)
+//   else:      dst (stride LDX) = out (in place allowed: each wave reads its rows before writing)
+// The fragments are loaded one phase ahead (gfrag_load) so their L2 latency hides there.
+struct GFrag {
+    float lb[5], l16[5];
+};
+__device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int lane) {
+    GFrag f;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        f.lb[s] = LF[s * 64 + lane];
+        f.l16[s] = LF[(5 + s) * 64 + lane];
+    }
+    return f;
+}
+
+template <bool RESID, bool SPLIT_OUT = false>
+__device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, float* dst,
+                                          const float* __restrict__ bias, int wave, int lane) {
+    lane = opaque(lane);
+    if (wave >= P) return;
+    const int g = lane >> 4, cl = lane & 15;
+    const float(&lb)[5] = f.lb;
+    const float(&l16)[5] = f.l16;
+    const float* xp = src + wave * J * LDX + cl;
+    float a[6][5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int row = min(4 * s + g, J - 1);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) a[t][s] = xp[row * LDX + 16 * t];
+    }
+    f32x4 acc[6];
+    float p16[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        p16[t] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], lb[s], acc[t], 0, 0, 0);
+            p16[t] = fmaf(l16[s], a[t][s], p16[t]);
+        }
+    }
+    const int row_j = wave * J + cl, row16 = wave * J + 16;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        const int c0 = 16 * t + 4 * g;
+        if constexpr (SPLIT_OUT) {
+            split_store4(reinterpret_cast<char*>(dst + row_j * LD2), c0, acc[t]);
+        } else if constexpr (RESID) {
+            f32x4* o = reinterpret_cast<f32x4*>(dst + row_j * LDX + c0);
+            *o = *o + (acc[t] + *reinterpret_cast<const f32x4*>(bias + c0));
+        } else {
+            *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = acc[t];
+        }
+    }
+    float v16[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) v16[t] = sum4rows(p16[t]);
+    if (g == 0) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const int c = 16 * t + cl;
+            if constexpr (SPLIT_OUT) {
+                split_store1(reinterpret_cast<char*>(dst + row16 * LD2), c, v16[t]);
+            } else if constexpr (RESID) {
+                dst[row16 * LDX + c] = dst[row16 * LDX + c] + (v16[t] + bias[c]);
+            } else {
+                dst[row16 * LDX + c] = v16[t];
+            }
         }
     }
 }
@@ -1456,9 +1546,10 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             //      fc2's split A operand into B2[:, 96:288] (bytes 384..1152 of the row)
             if constexpr (G16) {
                 const auto pre = gemm16_prefetch<12, KB32_D>(L16 + O16_FC1, wave, lane);
+                const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
                 BAR();
-                if (DPK_RUN(2)) graph_op<false, true>(LW + OFF_LG, B1, B2, nullptr, tid);
+                if (DPK_RUN(2)) graph_mma<false, true>(gf, B1, B2, nullptr, wave, lane);
                 BAR();
                 if (DPK_RUN(16 | 128)) {
                     const EpiArgs e{B2 + D, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
@@ -1466,15 +1557,17 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 }
             } else {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
+                const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
                 BAR();
-                if (DPK_RUN(2)) graph_op<false>(LW + OFF_LG, B1, B1, nullptr, tid);
+                if (DPK_RUN(2)) graph_mma<false>(gf, B1, B1, nullptr, wave, lane);
                 BAR();
                 if (DPK_RUN(16 | 128)) {
                     const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
                     gemm_wg<12, 6, E_STORE_RELU>(B1, LDX, LW + OFF_FC1, wave, lane, e, pre);
                 }
             }
+            const GFrag gf2 = gfrag_load(LW + OFF_LGF, lane);   // graph2's operands, a GEMM ahead
             {
                 const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
@@ -1494,18 +1587,17 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 if constexpr (G16) {
                     const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C1, wave, lane);
                     BAR();
-                    if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
-                    BAR();
-                    // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj))
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, XS, B2, tid);
+                    if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
+                    // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj));
+                    //      cheb_prep reads only its own wave's rows of XS (wave = pose): no barrier
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, XS, B2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 512)) gemm_wg16<6, KB32_D3, E_CHEB1, false>(B2b, LD2 * 4, L16 + O16_C1, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
                     BAR();
-                    if (DPK_RUN(2)) graph_op<true>(LW + OFF_LG, B1, XS, LW + OFF_BFC2, tid);
-                    BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, tid);
+                    if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 512)) gemm_wg<6, 18, E_CHEB1>(B2, LD2, LW + OFF_C1, wave, lane, e, pre);
                 }
@@ -1515,14 +1607,14 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 if constexpr (G16) {
                     const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C2, wave, lane);
                     BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, B1, B2, tid);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, B1, B2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 1024))
                         gemm_wg16<6, KB32_D3, E_RESID_RELU, false>(B2b, LD2 * 4, L16 + O16_C2, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
                     BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, tid);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 1024)) gemm_wg<6, 18, E_RESID_RELU>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
                 }
@@ -1532,7 +1624,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
         //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly)
         const auto preo = out_prefetch<18>(W + OFF_WOUT, lane);
-        cheb_prep<SPARSE>(CW, XS, B2, tid);
+        cheb_prep<SPARSE>(CW, XS, B2, wave, lane);
         BAR();
         {
             float cf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2017,6 +2109,12 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         }
         for (int c = 0; c < D2; ++c) Lw[OFF_BFC1 + c] = f1b[c];
         graph_lap(ahat, Lw + OFF_LG);
+        for (int s = 0; s < 5; ++s)
+            for (int ln = 0; ln < 64; ++ln) {
+                const int i = 4 * s + (ln >> 4);
+                Lw[OFF_LGF + s * 64 + ln] = i < J ? Lw[OFF_LG + (ln & 15) * J + i] : 0.f;
+                Lw[OFF_LGF + (5 + s) * 64 + ln] = i < J ? Lw[OFF_LG + 16 * J + i] : 0.f;
+            }
         // temb_proj: transposed [in=384][out=96]
         if (!pose) {
             float* T = h->h_temb.data();

@@ -37,7 +37,7 @@ def _events(gemm_mode="fp32"):
         bar(p + "attention"); gemm(p + "O"); bar(p + "O")
         bar(p + "LN1"); bar(p + "graph1"); gemm(p + "fc1"); bar(p + "fc1")
         gemm(p + "fc2"); bar(p + "fc2")
-        bar(p + "graph2+b2"); bar(p + "cheb_prep1"); gemm(p + "C1"); bar(p + "C1")
+        bar(p + "graph2+cheb1"); gemm(p + "C1"); bar(p + "C1")
         bar(p + "cheb_prep2"); gemm(p + "C2"); bar(p + "C2")
     bar("cheb_out"); bar("out_gemm+ddim")
     return ev
