@@ -128,6 +128,27 @@ int dpk_pose(dpk_handle* h, const float* x2d_dev, float* xyz_dev, float* uvxyz_d
 int dpk_pose_metrics(const float* out_uvxyz_dev, const float* targets_dev, int F, int H, int root_mode,
                      double* p1_dev, double* p2_dev, float* xyz_dev, void* stream);
 
+/* GMM 2D-keypoint sampling of the input pipeline: replaces
+ * PoseGenerator_gmm.__getitem__ (common/generators.py:24-53) for a whole batch.
+ *   gmm_dev      [n_src,17,kernel_n,5] fp32  per joint: [w, mu_u, mu_v, var_u, var_v] x kernel_n
+ *   poses3d_dev  [n_src,17,3] fp32           3D poses (made root-relative here, generators.py:19)
+ *   index_dev    [F] int64 or NULL           source frame of each output (taken modulo n_src, as
+ *                                            generators.py:26-29); NULL = 0..F-1
+ *   u_dev        [F,17] fp64 or NULL         the uniform draw np.random.choice consumes for each
+ *                                            joint (RandomState.random_sample, in frame-then-joint
+ *                                            order); NULL = counter-based uniforms from `seed`
+ *   atol                                     numpy's tolerance on sum(w) = 1 (sqrt(eps) of the
+ *                                            weights' dtype: 3.4526698e-4 for float32)
+ *   uvxyz_dev, noise_scale_dev  [F,17,5] fp32 outputs (uvxyz = [mu_u, mu_v, xyz - xyz_root],
+ *                                            noise_scale = [var_u, var_v, 1, 1, 1])
+ *   status_dev   one int (device)            0, or an OR of 1 (a negative weight) and 2 (weights
+ *                                            not summing to 1 within atol): numpy's ValueErrors
+ * Component selection is numpy's RandomState.choice(kernel_n, 1, p) bit for bit given u.
+ * Returns DPK_OK, DPK_E_INVALID (kernel_n outside 1..64, bad pointers) or DPK_E_HIP. */
+int dpk_gmm_sample(const float* gmm_dev, const float* poses3d_dev, int n_src, int kernel_n,
+                   const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
+                   float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream);
+
 /* GEMM arithmetic of the sampler's transformer/ResChebGC GEMMs (not part of the reference
  * interface; the reference computes everything in fp32 on its device):
  *   mode 0 (default): fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 accumulate;

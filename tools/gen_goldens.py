@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
-    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g7); default all")
+    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g8); default all")
     args = ap.parse_args()
     only = set(x for x in args.only.split(",") if x)
 
@@ -221,6 +221,38 @@ def main():
                  p1=np.float64(p1), p2=np.float64(p2), action_names=np.array(names),
                  action_p1=np.array([err[a]["p1"].avg for a in names], dtype=np.float64),
                  action_p2=np.array([err[a]["p2"].avg for a in names], dtype=np.float64))
+
+    # ---------------- G8: GMM input sampler (common/generators.py) ----------------
+    if want("g8"):
+        from common.generators import PoseGenerator_gmm
+
+        rng = np.random.Generator(np.random.PCG64(4242))
+        lens, kn = (7, 5, 9), 5
+        p3s, gms, acts, cams = [], [], [], []
+        for si, n in enumerate(lens):
+            w = rng.dirichlet(np.ones(kn), size=(n, 17))
+            w[0, 0] = [1, 0, 0, 0, 0]                # one-hot rows and interior zeros
+            w[0, 1] = [0, 0, 0, 0, 1]
+            w[1, 2] = [0.5, 0, 0.25, 0, 0.25]
+            g = np.empty((n, 17, kn, 5))
+            g[..., 0] = w
+            g[..., 1:3] = rng.uniform(-1, 1, size=(n, 17, kn, 2))
+            g[..., 3:5] = rng.uniform(1e-4, 1e-2, size=(n, 17, kn, 2))
+            gms.append(g.astype(np.float32))
+            p3s.append(rng.normal(0.0, 0.4, size=(n, 17, 3)).astype(np.float32) + np.float32(si))
+            acts.append([f"Walking {si}"] * n)
+            cams.append(rng.normal(size=(n, 9)).astype(np.float32))
+        ds = PoseGenerator_gmm([a.copy() for a in p3s], [a.copy() for a in gms], acts, cams)
+        indices = [0, 3, 20, 7, 21, 13, 5, 20, 1]
+        np.random.seed(2024)
+        items = [ds[i] for i in indices]
+        np.random.seed(2024)
+        u = np.random.random_sample((len(indices), 17))
+        np.savez(os.path.join(args.out, "g8_gmm.npz"), poses_3d=np.concatenate(p3s), gmm=np.concatenate(gms),
+                 lens=np.array(lens), indices=np.array(indices), u=u,
+                 uvxyz=np.stack([it[0].numpy() for it in items]), noise_scale=np.stack([it[1].numpy() for it in items]),
+                 pose_2d=np.stack([it[2].numpy() for it in items]), pose_3d=np.stack([it[3].numpy() for it in items]),
+                 actions=np.array([it[4] for it in items]), camerapara=np.stack([it[5].numpy() for it in items]))
 
     with open(os.path.join(args.out, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
