@@ -14,7 +14,10 @@ Also reported on the same JSON line:
   cpu_baseline  the golden-pinned oracle (torch CPU, the reference's op sequence) timed on
                 this host's cores on the first --cpu-frames frames of the same batch (rank 0,
                 N=1 only);
-  parity        MPJPE (mm) of the HIP result vs the oracle on those frames, and max |diff|.
+  parity        MPJPE (mm) of the HIP result vs the oracle on those frames, and max |diff|;
+  variants      the same measurement (warmup, timed steps, roofline, parity) in the other GEMM
+                mode: the headline is fp32 MFMA (the reference's arithmetic); "f16x3" runs the
+                layer GEMMs as three fp16-split MFMA products with fp32 accumulation.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -52,7 +55,9 @@ def parse():
     ap.add_argument("--cpu-repeats", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gemm", choices=("fp32", "f16x3"), default="fp32",
-                    help="per-layer GEMM arithmetic (dpk_set_gemm_mode); fp32 is the reference's")
+                    help="per-layer GEMM arithmetic of the headline (dpk_set_gemm_mode); fp32 is the reference's")
+    ap.add_argument("--no-variants", dest="variants", action="store_false",
+                    help="skip timing the other GEMM mode (reported under 'variants')")
     return ap.parse_args()
 
 
@@ -98,7 +103,6 @@ def main():
     # ---- model, schedule, inputs (synthetic, seeded) ----
     model = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
     model.load_state_dict(synthetic_state_dict())
-    model.set_gemm_mode(args.gemm)
     seq = make_seq("uniform", args.T_test, args.K)
     betas = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
                                                num_diffusion_timesteps=args.T)).float()
@@ -117,64 +121,86 @@ def main():
         if world > 1:                            # the one data-path collective: final poses to every rank
             D.gather_frames(out, B_total, args.hyp)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            step()                                   # warm the side stream
-        torch.cuda.current_stream(dev).wait_stream(s)
-        torch.cuda.synchronize()
-        with torch.cuda.graph(graph):
+    def measure(gemm):
+        """Time exactly args.steps steps (barrier + sync both sides, max over ranks) in one GEMM mode."""
+        model.set_gemm_mode(gemm)
+        for _ in range(args.warmup):
             step()
-        run = graph.replay
-    else:
-        run = step
-        model.profile(True)
+        torch.cuda.synchronize()
+        graph = None
+        if args.graph:
+            graph = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                step()                                   # warm the side stream
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph):
+                step()
+            run = graph.replay
+        else:
+            run = step
+            model.profile(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+        kernel_ms = model.kernel_times_ms() if graph is None else []
+        model.profile(False)
+        return elapsed, kernel_ms
 
-    # ---- timed region: barrier + sync on both sides, max over ranks ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
-    kernel_ms = model.kernel_times_ms() if graph is None else []
-    model.profile(False)
-
-    frames_done = B_total * args.steps
-    value = frames_done / elapsed
-    ms_per_step = elapsed / args.steps * 1000.0
-    avg_kernel_ms = float(np.mean(kernel_ms)) if kernel_ms else None
-    roof = None
-    if avg_kernel_ms:
+    def roofline(gemm, kernel_ms):
+        if not kernel_ms:
+            return None
+        avg_kernel_ms = float(np.mean(kernel_ms))
         achieved = W_ALG * rows * K / (avg_kernel_ms * 1e-3) / 1e12
         # f16x3: every fp32 product is three f16 MFMA passes, so the fp32-equivalent peak is 1/3 of f16's
-        peak = PEAK_FP32_MFMA if args.gemm == "fp32" else round(PEAK_F16_MFMA / 3, 1)
+        peak = PEAK_FP32_MFMA if gemm == "fp32" else round(PEAK_F16_MFMA / 3, 1)
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": "dpk::sample_kernel<0, *, %s>" % ("false" if args.gemm == "fp32" else "true"), "avg_launch_ms": round(avg_kernel_ms, 4),
+                "kernel": "dpk::sample_kernel<0, *, %s>" % ("false" if gemm == "fp32" else "true"),
+                "avg_launch_ms": round(avg_kernel_ms, 4),
                 "launches": len(kernel_ms), "flop_per_launch": W_ALG * rows * K,
                 "per_unit": f"{W_ALG} FLOP per pose-step (SURVEY 8d) x {rows} poses x {K} steps"}
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
             try:
                 tr = json.load(open(tfile))
-                key = f"frames{args.frames}_hyp{args.hyp}_K{K}" + ("" if args.gemm == "fp32" else "_" + args.gemm)
+                key = f"frames{args.frames}_hyp{args.hyp}_K{K}" + ("" if gemm == "fp32" else "_" + gemm)
                 if key in tr:
                     roof["traffic"] = tr[key]["hbm_bytes_per_launch"]
                     roof["traffic_source"] = tr[key]["source"]
             except (OSError, ValueError, KeyError):
                 pass
+        return roof
+
+    # ---- timed region (headline mode), then the other GEMM mode as a variant on the same line ----
+    elapsed, kernel_ms = measure(args.gemm)
+    out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0) else None
+    variants = {}
+    if args.variants:
+        for g in ("fp32", "f16x3"):
+            if g == args.gemm:
+                continue
+            e2, k2 = measure(g)
+            variants[g] = {"value": round(B_total * args.steps / e2, 2), "ms_per_step": round(e2 / args.steps * 1e3, 4),
+                           "roofline": roofline(g, k2),
+                           "dtype": "fp32" if g == "fp32" else "fp32 (layer GEMMs as 3x fp16-split MFMA, fp32 accumulate)"}
+            if world == 1 and rank == 0:
+                variants[g]["_out"] = out.detach().cpu().numpy()
+        model.set_gemm_mode(args.gemm)
+
+    frames_done = B_total * args.steps
+    value = frames_done / elapsed
+    ms_per_step = elapsed / args.steps * 1000.0
+    roof = roofline(args.gemm, kernel_ms)
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
@@ -190,6 +216,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if variants:
+        result["variants"] = variants
     if args.hyp > 1:
         result["rows_per_s"] = round(value * args.hyp, 2)
 
@@ -221,14 +249,22 @@ def main():
                       f"{os.cpu_count()} logical CPUs, {cores} threads"}
         if args.eta == 0.0:
             idx = np.concatenate([np.arange(h * args.frames, h * args.frames + n_cpu) for h in range(args.hyp)])
-            hip_out = out.detach().cpu().numpy()[idx]
             ref_np = ref.numpy()
             tg = tgt_all[:n_cpu]
-            m_h, m_r = mpjpe_mm(hip_out, tg, args.hyp), mpjpe_mm(ref_np, tg, args.hyp)
-            result["parity"] = {"frames": n_cpu, "mpjpe_hip_mm": round(m_h, 6), "mpjpe_ref_mm": round(m_r, 6),
-                                "mpjpe_delta_mm": float(f"{abs(m_h - m_r):.3e}"),
-                                "max_abs_diff": float(f"{float(np.abs(hip_out - ref_np).max()):.3e}"),
-                                "tolerance_mm": 1e-4, "pass": abs(m_h - m_r) <= 1e-4}
+            m_r = mpjpe_mm(ref_np, tg, args.hyp)
+
+            def parity(full_out):
+                hip_out = full_out[idx]
+                m_h = mpjpe_mm(hip_out, tg, args.hyp)
+                return {"frames": n_cpu, "mpjpe_hip_mm": round(m_h, 6), "mpjpe_ref_mm": round(m_r, 6),
+                        "mpjpe_delta_mm": float(f"{abs(m_h - m_r):.3e}"),
+                        "max_abs_diff": float(f"{float(np.abs(hip_out - ref_np).max()):.3e}"),
+                        "tolerance_mm": 1e-4, "pass": abs(m_h - m_r) <= 1e-4}
+            result["parity"] = parity(out_main)
+            for v in variants.values():
+                v["parity"] = parity(v["_out"])
+    for v in variants.values():
+        v.pop("_out", None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

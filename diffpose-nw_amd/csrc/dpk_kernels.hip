@@ -83,6 +83,9 @@ constexpr int COUT = 5;      // coords_dim[1]
 constexpr int PE = J * CIN;  // floats per pose (85)
 
 // workgroup tile
+#ifndef DPK_ATTN_MMA
+#define DPK_ATTN_MMA 1       // attention on the matrix cores (attention_mma) or on DPP rows (attention)
+#endif
 #ifndef DPK_P
 #define DPK_P 4              // poses per workgroup: 4 (one workgroup per CU) or 2 (two per CU)
 #endif
@@ -275,10 +278,10 @@ __device__ __forceinline__ void ddim_elem(const float* cf, float xt, float et, f
 // two LDS-crossbar shuffles.
 __device__ __forceinline__ float sum4rows(float v) {
     float a = v, b = v;
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
     const float s1 = a + b;
     float c = s1, d = s1;
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
     return c + d;
 }
 
@@ -1177,6 +1180,216 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
     }
 }
 
+// Max over the 4 lane rows (l, l^16, l^32, l^48), result in every lane (cf. sum4rows).
+__device__ __forceinline__ float max4rows(float v) {
+    float a = v, b = v;
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    const float s1 = fmaxf(a, b);
+    float c = s1, d = s1;
+    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
+    return fmaxf(c, d);
+}
+
+// The same attention on the matrix cores (v_mfma_f32_16x16x4_f32).  Wave w = pose w, the 4
+// heads in turn.  Lane (g = l>>4, c = l&15) loads query/key row c at its 6 feature dims
+// {4g..4g+3, 16+2g, 17+2g}, the k-slice it feeds to the MFMAs, so:
+//   scores   S^T = K Q^T   (6 MFMAs): lane (g, c) ends with S[query c][keys 4g..4g+3];
+//   key 16 / query 16      per-lane partial dot products over the lane's dims, summed over
+//                          the 4 lane rows (permlane), so lane (g, c) also holds S[c][16],
+//                          S[16][c] and S[16][16];
+//   softmax  per query c: its 4 keys in registers, max/sum over the lane rows by permlane;
+//   P.V      O^T = V^T P^T (4 MFMAs per 16-wide column tile; lane row g feeds keys 4g..4g+3,
+//            the permuted order the scores left them in), so lane (g, c) ends with
+//            O[query c][dims 4g..4g+3] of the tile: one 16-byte store; key 16 added by FMA;
+//   query 16 lane (g, c) forms p16[c] * V[c][6g..6g+5], summed over the DPP row.
+// Same arithmetic as the reference (scores / sqrt(d_k) by correctly rounded division,
+// masked keys -1e9, softmax, P.V), fp32 throughout; only the summation orders differ.
+template <bool SPLIT = false>
+__device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsigned mask, int wave, int lane) {
+    lane = opaque(lane);
+    if (wave >= P) return;
+    const int g = lane >> 4, c = lane & 15;
+    const float rcp_sdk = 1.0f / SQRT_DK;
+    constexpr float LOG2E = 1.4426950408889634f;
+    const float* prow = qkv + wave * J * LD2;
+    float* orow = out + wave * J * LDX;
+    const bool kok16 = ((mask >> 16) & 1u) != 0u;
+    bool kokr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kokr[r] = ((mask >> (4 * g + r)) & 1u) != 0u;
+    // scores / sqrt(d_k), masked keys -1e9 (GraFormer.py:104-106); exp as 2^(x log2 e) on
+    // v_exp_f32 (the softmax's max is subtracted first, so x <= 0)
+    auto scale = [&](float dot, bool ok) { return ok ? dot * rcp_sdk : -1e9f; };
+    auto ex = [&](float x) { return __builtin_amdgcn_exp2f(x * LOG2E); };
+    // The 4 heads are independent: every stage below runs over all of them before the next
+    // stage, so the in-order issue interleaves 4 dependency chains (MFMA accumulations,
+    // permlane reductions, exp) instead of waiting out one head's latencies at a time.
+    f32x4 q4[NH], k4[NH], Q4[NH], K4[NH], V4a[NH], V4b[NH];
+    f32x2 q2[NH], k2[NH], Q2[NH], K2[NH];
+    float va[NH][4], vb[NH][4];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const float* rc = prow + h * DK + c * LD2;
+        const float* r16 = prow + h * DK + 16 * LD2;
+        q4[h] = *reinterpret_cast<const f32x4*>(rc + 4 * g);
+        q2[h] = *reinterpret_cast<const f32x2*>(rc + 16 + 2 * g);
+        k4[h] = *reinterpret_cast<const f32x4*>(rc + D + 4 * g);
+        k2[h] = *reinterpret_cast<const f32x2*>(rc + D + 16 + 2 * g);
+        Q4[h] = *reinterpret_cast<const f32x4*>(r16 + 4 * g);
+        Q2[h] = *reinterpret_cast<const f32x2*>(r16 + 16 + 2 * g);
+        K4[h] = *reinterpret_cast<const f32x4*>(r16 + D + 4 * g);
+        K2[h] = *reinterpret_cast<const f32x2*>(r16 + D + 16 + 2 * g);
+    }
+    // ---- scores S^T = K Q^T and, with query 16's row broadcast to every column,
+    //      S16 = K q16 (6 MFMAs each per head): lane (g, c) holds S[c][4g+r] and S[16][4g+r]
+    f32x4 st[NH], st16[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        st[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st16[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const float kk = m < 4 ? k4[h][m & 3] : k2[h][m & 1];
+            st[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? q4[h][m & 3] : q2[h][m & 1], st[h], 0, 0, 0);
+            st16[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? Q4[h][m & 3] : Q2[h][m & 1], st16[h], 0, 0, 0);
+        }
+    // V operands: column tile 0 (dims 0..15) and 1 (dims 16..23; rows c >= 8 duplicate, unused)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const float* vbase = prow + h * DK + 2 * D;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            va[h][r] = vbase[(4 * g + r) * LD2 + c];
+            vb[h][r] = vbase[(4 * g + r) * LD2 + 16 + (c & 7)];
+        }
+        V4a[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 4 * g);
+        V4b[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 16 + 4 * (g & 1));
+    }
+    // ---- key 16 by partial dots over this lane's 6 dims, summed over the lane rows:
+    //      S[c][16] and S[16][16]
+    float s_c16[NH], s_1616[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        float pa = 0.f, pc = 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            pa = fmaf(q4[h][m], K4[h][m], pa);
+            pc = fmaf(Q4[h][m], K4[h][m], pc);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            pa = fmaf(q2[h][m], K2[h][m], pa);
+            pc = fmaf(Q2[h][m], K2[h][m], pc);
+        }
+        s_c16[h] = pa;
+        s_1616[h] = pc;
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        s_c16[h] = scale(sum4rows(s_c16[h]), kok16);
+        s_1616[h] = scale(sum4rows(s_1616[h]), kok16);
+    }
+    // ---- softmax of query c and of query 16 over keys 4g+r (this lane) and 16
+    float p[NH][4], p16[NH], u[NH][4], u16[NH], mx[NH], my[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            p[h][r] = scale(st[h][r], kokr[r]);
+            u[h][r] = scale(st16[h][r], kokr[r]);
+        }
+        mx[h] = fmaxf(fmaxf(p[h][0], p[h][1]), fmaxf(p[h][2], p[h][3]));
+        my[h] = fmaxf(fmaxf(u[h][0], u[h][1]), fmaxf(u[h][2], u[h][3]));
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        mx[h] = fmaxf(max4rows(mx[h]), s_c16[h]);
+        my[h] = fmaxf(max4rows(my[h]), s_1616[h]);
+    }
+    float sum[NH], sum16[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            p[h][r] = ex(p[h][r] - mx[h]);
+            u[h][r] = ex(u[h][r] - my[h]);
+        }
+        p16[h] = ex(s_c16[h] - mx[h]);
+        u16[h] = ex(s_1616[h] - my[h]);
+        sum[h] = (p[h][0] + p[h][1]) + (p[h][2] + p[h][3]);
+        sum16[h] = (u[h][0] + u[h][1]) + (u[h][2] + u[h][3]);
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        sum[h] = sum4rows(sum[h]) + p16[h];
+        sum16[h] = sum4rows(sum16[h]) + u16[h];
+    }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        const float rs = __builtin_amdgcn_rcpf(sum[h]), rs16 = __builtin_amdgcn_rcpf(sum16[h]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            p[h][r] *= rs;
+            u[h][r] *= rs16;
+        }
+        p16[h] *= rs;
+        u16[h] *= rs16;
+    }
+    // ---- O^T = V^T P^T over keys 0..15 (4 MFMAs per column tile), then key 16 by FMA;
+    //      query 16: this lane's keys 4g+r against V columns c and 16+c, summed over lane rows
+    f32x4 oa[NH], ob[NH];
+    float ya[NH], yb[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        oa[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ob[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ya[h] = 0.f;
+        yb[h] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            oa[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[h][r], p[h][r], oa[h], 0, 0, 0);
+            ob[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[h][r], p[h][r], ob[h], 0, 0, 0);
+            ya[h] = fmaf(u[h][r], va[h][r], ya[h]);
+            yb[h] = fmaf(u[h][r], vb[h][r], yb[h]);
+        }
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        ya[h] = sum4rows(ya[h]);
+        yb[h] = sum4rows(yb[h]);
+    }
+    // ---- stores: O[c][h*24 + 4g..] (tile 0), O[c][h*24 + 16 + 4g..] (tile 1, g < 2);
+    //      O[16][h*24 + c] and O[16][h*24 + 16 + c] (c < 8) from lane row 0
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            oa[h][r] = fmaf(p16[h], V4a[h][r], oa[h][r]);
+            ob[h][r] = fmaf(p16[h], V4b[h][r], ob[h][r]);
+        }
+        const float* v16 = prow + h * DK + 16 * LD2 + 2 * D;
+        const int col = h * DK;
+        if constexpr (SPLIT) {
+            char* rowc = reinterpret_cast<char*>(orow + c * LDX);
+            char* row16 = reinterpret_cast<char*>(orow + 16 * LDX);
+            split_store4(rowc, col + 4 * g, oa[h]);
+            if (g < 2) split_store4(rowc, col + 16 + 4 * g, ob[h]);
+            if (g == 0) split_store1(row16, col + c, fmaf(u16[h], v16[c], ya[h]));
+            if (g == 1 && c < 8) split_store1(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]));
+        } else {
+            *reinterpret_cast<f32x4*>(orow + c * LDX + col + 4 * g) = oa[h];
+            if (g < 2) *reinterpret_cast<f32x4*>(orow + c * LDX + col + 16 + 4 * g) = ob[h];
+            if (g == 0) orow[16 * LDX + col + c] = fmaf(u16[h], v16[c], ya[h]);
+            if (g == 1 && c < 8) orow[16 * LDX + col + 16 + c] = fmaf(u16[h], v16[16 + c], yb[h]);
+        }
+    }
+}
+
 // --- graph products -------------------------------------------------------------------
 // Chebyshev terms T1 = L, T2 = 2L^2 - I of the H36M skeleton (runners/diffpose_frame.py:120-124)
 // are sparse (49 / 87 of 289 entries).  Their pattern is derived here at compile time from the
@@ -1529,12 +1742,18 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
                     const auto pre = gemm16_prefetch<6, KB32_D>(L16 + O16_O, wave, lane);
-                    if (DPK_RUN(1)) attention<true>(B2, B1, a.mask, tid);
+                    if (DPK_RUN(1)) {
+                        if constexpr (DPK_ATTN_MMA) attention_mma<true>(B2, B1, a.mask, wave, lane);
+                        else attention<true>(B2, B1, a.mask, tid);
+                    }
                     BAR();
                     if (DPK_RUN(16 | 64)) gemm_wg16<6, KB32_D, E_RESID, false>(B1b, LDX * 4, L16 + O16_O, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
-                    if (DPK_RUN(1)) attention(B2, B1, a.mask, tid);
+                    if (DPK_RUN(1)) {
+                        if constexpr (DPK_ATTN_MMA) attention_mma(B2, B1, a.mask, wave, lane);
+                        else attention(B2, B1, a.mask, tid);
+                    }
                     BAR();
                     if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
                 }

@@ -45,7 +45,7 @@ def _events(gemm_mode="fp32"):
 
 def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
-    src = [os.path.join(ROOT, "diffpose-nw_amd", "csrc", f) for f in ("dpk_kernels.hip", "dpk_metrics.hip")]
+    src = [os.path.join(ROOT, "diffpose-nw_amd", "csrc", f) for f in ("dpk_kernels.hip", "dpk_metrics.hip", "dpk_gmm.hip")]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-fno-slp-vectorize", "-Wno-unused-result", f"-I{ROOT}/include", "-DDPK_TRACE=1"] + src + ["-o", SO]
     cmd += os.environ.get("DPK_TRACE_EXTRA", "").split()
