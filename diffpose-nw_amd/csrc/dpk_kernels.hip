@@ -179,32 +179,48 @@ __device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split_f16(f32x2 v, f16x2& hi, f16x2& lo) {
-    hi = __builtin_convertvector(v, f16x2);
-    lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x2), f16x2);
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+// SP = 1: hi/lo fp16 pair (gemm mode 1, split-fp16); SP = 2: hi/lo bf16 pair (gemm mode 2,
+// bf16 GEMMs, which read only the hi half).  Both keep the same 32-byte chunk layout.
+template <int SP>
+__device__ __forceinline__ void split_pair(f32x2 v, f16x2& hi, f16x2& lo) {
+    if constexpr (SP == 2) {
+        const bf16x2 h = __builtin_convertvector(v, bf16x2);
+        const bf16x2 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), bf16x2);
+        hi = __builtin_bit_cast(f16x2, h);
+        lo = __builtin_bit_cast(f16x2, l);
+    } else {
+        hi = __builtin_convertvector(v, f16x2);
+        lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x2), f16x2);
+    }
 }
 // 4 consecutive columns col..col+3 (col % 4 == 0) of a split row
+template <int SP>
 __device__ __forceinline__ void split_store4(char* row, int col, f32x4 v) {
     f16x2 h0, l0, h1, l1;
-    split_f16(f32x2{v[0], v[1]}, h0, l0);
-    split_f16(f32x2{v[2], v[3]}, h1, l1);
+    split_pair<SP>(f32x2{v[0], v[1]}, h0, l0);
+    split_pair<SP>(f32x2{v[2], v[3]}, h1, l1);
     char* p = row + (col >> 3) * 32 + (col & 7) * 2;
     *reinterpret_cast<f16x4*>(p) = f16x4{h0[0], h0[1], h1[0], h1[1]};
     *reinterpret_cast<f16x4*>(p + 16) = f16x4{l0[0], l0[1], l1[0], l1[1]};
 }
+template <int SP>
 __device__ __forceinline__ void split_store2(char* row, int col, f32x2 v) {   // col % 2 == 0
     f16x2 h, l;
-    split_f16(v, h, l);
+    split_pair<SP>(v, h, l);
     char* p = row + (col >> 3) * 32 + (col & 7) * 2;
     *reinterpret_cast<f16x2*>(p) = h;
     *reinterpret_cast<f16x2*>(p + 16) = l;
 }
+template <int SP>
 __device__ __forceinline__ void split_store1(char* row, int col, float v) {
-    const _Float16 h = (_Float16)v;
-    const _Float16 l = (_Float16)(v - (float)h);
+    f16x2 h, l;
+    split_pair<SP>(f32x2{v, 0.f}, h, l);
     char* p = row + (col >> 3) * 32 + (col & 7) * 2;
-    *reinterpret_cast<_Float16*>(p) = h;
-    *reinterpret_cast<_Float16*>(p + 16) = l;
+    *reinterpret_cast<_Float16*>(p) = h[0];
+    *reinterpret_cast<_Float16*>(p + 16) = l[0];
 }
 
 // Kernel modes: the K-step sampler (GCNdiff + DDIM), one GCNdiff eps evaluation, or one
@@ -680,7 +696,7 @@ __device__ __forceinline__ int pass_col(int ctp, int c, int rot) {
 }
 
 // first two k-blocks of the wave's first pass (issued before the preceding VALU phase)
-template <int NC, int KB32>
+template <int G, int NC, int KB32>
 __device__ __forceinline__ BPre16<PW16> gemm16_prefetch(const char* Bp, int wave, int lane) {
     constexpr int NCW = NC / 2;
     const BSrc16 s = bsrc16<NC, KB32>(Bp, lane);
@@ -690,9 +706,11 @@ __device__ __forceinline__ BPre16<PW16> gemm16_prefetch(const char* Bp, int wave
     for (int c = 0; c < PW16; ++c) {
         const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
         pre.h0[c] = s.load(b0);
-        pre.l0[c] = s.load(b0 + 1024);
         pre.h1[c] = s.load(b0 + BLK16);
-        pre.l1[c] = s.load(b0 + BLK16 + 1024);
+        if constexpr (G == 1) {
+            pre.l0[c] = s.load(b0 + 1024);
+            pre.l1[c] = s.load(b0 + BLK16 + 1024);
+        }
     }
     return pre;
 }
@@ -700,7 +718,7 @@ __device__ __forceinline__ BPre16<PW16> gemm16_prefetch(const char* Bp, int wave
 __device__ __forceinline__ f16x4 half_lo(f16x8 v) { return __builtin_shufflevector(v, v, 0, 1, 2, 3); }
 __device__ __forceinline__ f16x4 half_hi(f16x8 v) { return __builtin_shufflevector(v, v, 4, 5, 6, 7); }
 
-template <int NR, int PW, int NC, int KB32, int MODE, bool OUTSPLIT>
+template <int G, int NR, int PW, int NC, int KB32, int MODE, int OUTSPLIT>
 __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16& src, int rt0, int ctp, int rot,
                                             int trow0, bool tail_dup, int lane, const EpiArgs& e,
                                             const BPre16<PW>& pre) {
@@ -752,10 +770,10 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             ah[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128);
-            al[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128 + 16);
+            if constexpr (G == 1) al[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128 + 16);
         }
         th[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128);
-        tl[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128 + 16);
+        if constexpr (G == 1) tl[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128 + 16);
     };
     loadA(0, 0);
     if constexpr (KB32 > 1) loadA(1, 1);
@@ -763,32 +781,49 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
     for (int kb = 0; kb < KB32; ++kb) {
         const int st = kb & 1;
         // transposed tiles: weight fragment as the A operand (cf. GemmTile TRANS)
+        if constexpr (G == 2) {
+            // bf16 (gemm mode 2): one product per tile, hi halves only
 #pragma unroll
-        for (int i = 0; i < NR; ++i)
+            for (int i = 0; i < NR; ++i)
 #pragma unroll
-            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[st][c], ah[st][i], acc[i][c], 0, 0, 0);
+                for (int c = 0; c < PW; ++c)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bh[st][c]),
+                                                                        __builtin_bit_cast(bf16x8, ah[st][i]), acc[i][c], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], al[st][i], acc[i][c], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], ah[st][i], acc[i][c], 0, 0, 0);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bl[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bl[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(tl[st]), tacc[q], 0, 0, 0);
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(tl[st]), tacc[q], 0, 0, 0);
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
-            tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
-        }
+            for (int q = 0; q < NQ; ++q) {
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(__builtin_bit_cast(s16x4, half_lo(bh[st][q])),
+                                                                 __builtin_bit_cast(s16x4, half_lo(th[st])), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(__builtin_bit_cast(s16x4, half_hi(bh[st][q])),
+                                                                 __builtin_bit_cast(s16x4, half_hi(th[st])), tacc[q], 0, 0, 0);
+            }
+        } else {
+    #pragma unroll
+            for (int i = 0; i < NR; ++i)
+    #pragma unroll
+                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[st][c], ah[st][i], acc[i][c], 0, 0, 0);
+    #pragma unroll
+            for (int i = 0; i < NR; ++i)
+    #pragma unroll
+                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], al[st][i], acc[i][c], 0, 0, 0);
+    #pragma unroll
+            for (int i = 0; i < NR; ++i)
+    #pragma unroll
+                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], ah[st][i], acc[i][c], 0, 0, 0);
+    #pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bl[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bl[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(tl[st]), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(tl[st]), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
+                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
+            }
+}
         if (kb + 2 < KB32) {
 #pragma unroll
             for (int c = 0; c < PW; ++c) {
                 bh[st][c] = src.load(soff[c] + (kb + 2) * BLK16);
-                bl[st][c] = src.load(soff[c] + (kb + 2) * BLK16 + 1024);
+                if constexpr (G == 1) bl[st][c] = src.load(soff[c] + (kb + 2) * BLK16 + 1024);
             }
             loadA(st, kb + 2);
         }
@@ -804,7 +839,7 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
         return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
     };
     auto store = [&](int row, int col4, const f32x4& v) {
-        if constexpr (OUTSPLIT) split_store4(reinterpret_cast<char*>(e.dst + row * e.ldd), col4, v);
+        if constexpr (OUTSPLIT) split_store4<OUTSPLIT>(reinterpret_cast<char*>(e.dst + row * e.ldd), col4, v);
         else *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
     };
     f32x4 old[NR][PW];
@@ -838,7 +873,7 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
         const float oldt = RES ? e.dst[row * e.ldd + col] : 0.f;
         const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
         const float o = epi_value<MODE>(v * INV, tbias[q], tp, oldt);
-        if constexpr (OUTSPLIT) split_store1(reinterpret_cast<char*>(e.dst + row * e.ldd), col, o);
+        if constexpr (OUTSPLIT) split_store1<OUTSPLIT>(reinterpret_cast<char*>(e.dst + row * e.ldd), col, o);
         else e.dst[row * e.ldd + col] = o;
     }
     DPK_GEMM_HOOK(2);
@@ -846,7 +881,7 @@ __device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16
 
 // Whole-workgroup split-fp16 GEMM: same wave roles as gemm_wg; the wave's NC/2 column tiles in
 // passes of PW16.  A: split rows (bytes, stride lda); B: this GEMM's split weight blocks.
-template <int NC, int KB32, int MODE, bool OUTSPLIT>
+template <int G, int NC, int KB32, int MODE, int OUTSPLIT>
 __device__ __forceinline__ void gemm_wg16(const char* A, int lda, const char* Bp, int wave, int lane,
                                           const EpiArgs& e, const BPre16<PW16>& pre) {
     static_assert(NC % 2 == 0 && (NC / 2) % PW16 == 0 && (R == 68 || R == 34), "passes of 3 column tiles");
@@ -856,7 +891,7 @@ __device__ __forceinline__ void gemm_wg16(const char* A, int lda, const char* Bp
     const bool dup = (PW16 & 1) && pr == 1;
     const BSrc16 src = bsrc16<NC, KB32>(Bp, lane);
     DPK_GEMM_HOOK(0);
-    gemm16_pass<NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, gemm_ch(wave) * NCW, rot, R - R % 16, dup,
+    gemm16_pass<G, NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, gemm_ch(wave) * NCW, rot, R - R % 16, dup,
                                                      lane, e, pre);
 #pragma unroll 1
     for (int ps = 1; ps < NPASS; ++ps) {
@@ -866,11 +901,13 @@ __device__ __forceinline__ void gemm_wg16(const char* A, int lda, const char* Bp
         for (int c = 0; c < PW16; ++c) {
             const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
             p2.h0[c] = src.load(b0);
-            p2.l0[c] = src.load(b0 + 1024);
             p2.h1[c] = src.load(b0 + BLK16);
-            p2.l1[c] = src.load(b0 + BLK16 + 1024);
+            if constexpr (G == 1) {
+                p2.l0[c] = src.load(b0 + 1024);
+                p2.l1[c] = src.load(b0 + BLK16 + 1024);
+            }
         }
-        gemm16_pass<NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, ctp, rot, R - R % 16, dup, lane, e, p2);
+        gemm16_pass<G, NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, ctp, rot, R - R % 16, dup, lane, e, p2);
     }
 }
 
@@ -972,7 +1009,7 @@ __device__ __forceinline__ f32x2 div_by2(f32x2 x, float d, float r) {
     const f32x2 e = __builtin_elementwise_fma(-q, f32x2{d, d}, x);
     return __builtin_elementwise_fma(e, f32x2{r, r}, q);
 }
-template <bool SPLIT = false>
+template <int SPLIT = 0>
 __device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
                                            int tid) {
     tid = opaque(tid);
@@ -1026,7 +1063,7 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
         const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c0);
         const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c0);
         const f32x4 t = div_by4(gv * dv[e], den, rcp) + sv;
-        if constexpr (SPLIT) split_store4(reinterpret_cast<char*>(d), c0, t);
+        if constexpr (SPLIT) split_store4<SPLIT>(reinterpret_cast<char*>(d), c0, t);
         else *reinterpret_cast<f32x4*>(d + c0) = t;
     }
     if (lane < 16 && tail_ok) {
@@ -1037,7 +1074,7 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
             const f32x2 gv = *reinterpret_cast<const f32x2*>(gain + c0);
             const f32x2 sv = *reinterpret_cast<const f32x2*>(shift + c0);
             const f32x2 t = div_by2(gv * du[e], tden, trcp) + sv;
-            if constexpr (SPLIT) split_store2(reinterpret_cast<char*>(dt), c0, t);
+            if constexpr (SPLIT) split_store2<SPLIT>(reinterpret_cast<char*>(dt), c0, t);
             else *reinterpret_cast<f32x2*>(dt + c0) = t;
         }
     }
@@ -1076,7 +1113,7 @@ __device__ __forceinline__ void pv16_keys(float& o, float pj_row, const float* v
     if constexpr (J + 1 < 16) pv16_keys<J + 1>(o, pj_row, vcol);
 }
 
-template <bool SPLIT = false>
+template <int SPLIT = 0>
 __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
     tid = opaque(tid);
     const int grp = tid >> 4, q = tid & 15;
@@ -1138,7 +1175,7 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
 #pragma unroll
     for (int d = 0; d < DK; d += 4)
         if constexpr (SPLIT)
-            split_store4(reinterpret_cast<char*>(out + (p * J + q) * LDX), h * DK + d, f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]});
+            split_store4<SPLIT>(reinterpret_cast<char*>(out + (p * J + q) * LDX), h * DK + d, f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]});
         else
             *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
     // ---- query 16: lane j scores key j (its own key row); key 16 by every lane
@@ -1167,14 +1204,14 @@ __device__ __forceinline__ void attention(const float* qkv, float* out, unsigned
         pv16_keys<0>(o0, pq, vcol + q);
         o0 = fmaf(pk, vcol[16 * LD2 + q], o0);
         char* row16 = reinterpret_cast<char*>(out + (p * J + 16) * LDX);
-        if constexpr (SPLIT) split_store1(row16, h * DK + q, o0);
+        if constexpr (SPLIT) split_store1<SPLIT>(row16, h * DK + q, o0);
         else orows[16 * LDX + q] = o0;
         // all 16 lanes take part (the DPP broadcasts read every lane of the row); lanes q >= 8
         // read columns past the head (inside the row) and discard them
         pv16_keys<0>(o1, pq, vcol + q + 16);
         o1 = fmaf(pk, vcol[16 * LD2 + q + 16], o1);
         if (q < DK - 16) {
-            if constexpr (SPLIT) split_store1(row16, h * DK + q + 16, o1);
+            if constexpr (SPLIT) split_store1<SPLIT>(row16, h * DK + q + 16, o1);
             else orows[16 * LDX + q + 16] = o1;
         }
     }
@@ -1204,7 +1241,7 @@ __device__ __forceinline__ float max4rows(float v) {
 //   query 16 lane (g, c) forms p16[c] * V[c][6g..6g+5], summed over the DPP row.
 // Same arithmetic as the reference (scores / sqrt(d_k) by correctly rounded division,
 // masked keys -1e9, softmax, P.V), fp32 throughout; only the summation orders differ.
-template <bool SPLIT = false>
+template <int SPLIT = 0>
 __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsigned mask, int wave, int lane) {
     lane = opaque(lane);
     if (wave >= P) return;
@@ -1377,10 +1414,10 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
         if constexpr (SPLIT) {
             char* rowc = reinterpret_cast<char*>(orow + c * LDX);
             char* row16 = reinterpret_cast<char*>(orow + 16 * LDX);
-            split_store4(rowc, col + 4 * g, oa[h]);
-            if (g < 2) split_store4(rowc, col + 16 + 4 * g, ob[h]);
-            if (g == 0) split_store1(row16, col + c, fmaf(u16[h], v16[c], ya[h]));
-            if (g == 1 && c < 8) split_store1(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]));
+            split_store4<SPLIT>(rowc, col + 4 * g, oa[h]);
+            if (g < 2) split_store4<SPLIT>(rowc, col + 16 + 4 * g, ob[h]);
+            if (g == 0) split_store1<SPLIT>(row16, col + c, fmaf(u16[h], v16[c], ya[h]));
+            if (g == 1 && c < 8) split_store1<SPLIT>(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]));
         } else {
             *reinterpret_cast<f32x4*>(orow + c * LDX + col + 4 * g) = oa[h];
             if (g < 2) *reinterpret_cast<f32x4*>(orow + c * LDX + col + 16 + 4 * g) = ob[h];
@@ -1438,7 +1475,7 @@ static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 // earlier LDS writes produced when it follows graph_mma (no workgroup barrier in between).
 // SPARSE: compile-time pattern, packed values (scalar loads); dense: 17x17 from the arena.
 // Sums run over increasing i in both (identical bits).
-template <bool SPARSE, bool SPLIT = false>
+template <bool SPARSE, int SPLIT = 0>
 __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int wave,
                                           int lane) {
     lane = opaque(lane);
@@ -1468,9 +1505,9 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
         }
         if constexpr (SPLIT) {
             char* row = reinterpret_cast<char*>(b2 + (p * J + j) * LD2);
-            split_store2(row, c, t1);
-            split_store2(row, D + c, t2);
-            split_store2(row, 2 * D + c, v[j]);
+            split_store2<SPLIT>(row, c, t1);
+            split_store2<SPLIT>(row, D + c, t2);
+            split_store2<SPLIT>(row, 2 * D + c, v[j]);
         } else {
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
@@ -1485,7 +1522,7 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
 //   graph_resid:  xs[:, c] += L @ y[:, c] + bias[c]   (fc2 reordered: L (X1 W2^T) + b2)
 // SPLIT_OUT (gemm mode 1, graph1): the product is fc1's A operand and is written split-fp16
 // into rows of stride LD2 (B2) instead of fp32 in place.
-template <bool RESID, bool SPLIT_OUT = false>
+template <bool RESID, int SPLIT_OUT = 0>
 __device__ __forceinline__ void graph_op(const float* __restrict__ L, const float* src, float* dst,
                                          const float* __restrict__ bias, int tid) {
     tid = opaque(tid);
@@ -1504,7 +1541,7 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
 #pragma unroll
         for (int i = 0; i < J; ++i) acc = pfma(splat2(L[j * J + i]), v[i], acc);
         if constexpr (SPLIT_OUT) {
-            split_store2(reinterpret_cast<char*>(dst + (p * J + j) * LD2), c, acc);
+            split_store2<SPLIT_OUT>(reinterpret_cast<char*>(dst + (p * J + j) * LD2), c, acc);
             continue;
         }
         f32x2* o = reinterpret_cast<f32x2*>(dst + (p * J + j) * LDX + c);
@@ -1540,7 +1577,7 @@ __device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int la
     return f;
 }
 
-template <bool RESID, bool SPLIT_OUT = false>
+template <bool RESID, int SPLIT_OUT = 0>
 __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, float* dst,
                                           const float* __restrict__ bias, int wave, int lane) {
     lane = opaque(lane);
@@ -1573,7 +1610,7 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
     for (int t = 0; t < 6; ++t) {
         const int c0 = 16 * t + 4 * g;
         if constexpr (SPLIT_OUT) {
-            split_store4(reinterpret_cast<char*>(dst + row_j * LD2), c0, acc[t]);
+            split_store4<SPLIT_OUT>(reinterpret_cast<char*>(dst + row_j * LD2), c0, acc[t]);
         } else if constexpr (RESID) {
             f32x4* o = reinterpret_cast<f32x4*>(dst + row_j * LDX + c0);
             *o = *o + (acc[t] + *reinterpret_cast<const f32x4*>(bias + c0));
@@ -1589,7 +1626,7 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
         for (int t = 0; t < 6; ++t) {
             const int c = 16 * t + cl;
             if constexpr (SPLIT_OUT) {
-                split_store1(reinterpret_cast<char*>(dst + row16 * LD2), c, v16[t]);
+                split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c, v16[t]);
             } else if constexpr (RESID) {
                 dst[row16 * LDX + c] = dst[row16 * LDX + c] + (v16[t] + bias[c]);
             } else {
@@ -1635,7 +1672,7 @@ __device__ __forceinline__ void input_prep(const float* __restrict__ cw, const f
 // ---------------------------------------------------------------------------------------
 // The sampler: K DDIM steps (or one eps evaluation, or one GCNpose forward) for P poses
 // per workgroup.
-template <int MODE, bool SPARSE, bool G16>
+template <int MODE, bool SPARSE, int G16>
 // `arena` is a separate restrict kernel argument: the compiler can then prove the weight arena
 // is never written during the launch and turns its wave-uniform loads (Laplacians, Chebyshev
 // terms, LayerNorm gains, biases) into scalar s_load (in the SampleArgs struct it cannot, and
@@ -1726,10 +1763,10 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             {
                 const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<18, KB32_D>(L16 + O16_QKV, wave, lane);
-                    if (DPK_RUN(8)) layer_norm<true>(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
+                    const auto pre = gemm16_prefetch<G16, 18, KB32_D>(L16 + O16_QKV, wave, lane);
+                    if (DPK_RUN(8)) layer_norm<G16>(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
                     BAR();
-                    if (DPK_RUN(16 | 32)) gemm_wg16<18, KB32_D, E_STORE, false>(B1b, LDX * 4, L16 + O16_QKV, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 32)) gemm_wg16<G16, 18, KB32_D, E_STORE, 0>(B1b, LDX * 4, L16 + O16_QKV, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
                     if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
@@ -1741,13 +1778,13 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             {
                 const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<6, KB32_D>(L16 + O16_O, wave, lane);
+                    const auto pre = gemm16_prefetch<G16, 6, KB32_D>(L16 + O16_O, wave, lane);
                     if (DPK_RUN(1)) {
-                        if constexpr (DPK_ATTN_MMA) attention_mma<true>(B2, B1, a.mask, wave, lane);
-                        else attention<true>(B2, B1, a.mask, tid);
+                        if constexpr (DPK_ATTN_MMA) attention_mma<G16>(B2, B1, a.mask, wave, lane);
+                        else attention<G16>(B2, B1, a.mask, tid);
                     }
                     BAR();
-                    if (DPK_RUN(16 | 64)) gemm_wg16<6, KB32_D, E_RESID, false>(B1b, LDX * 4, L16 + O16_O, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 64)) gemm_wg16<G16, 6, KB32_D, E_RESID, 0>(B1b, LDX * 4, L16 + O16_O, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
                     if (DPK_RUN(1)) {
@@ -1764,15 +1801,15 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             //      split path: graph1 writes fc1's A operand split into B2[:, 0:96]; fc1 writes
             //      fc2's split A operand into B2[:, 96:288] (bytes 384..1152 of the row)
             if constexpr (G16) {
-                const auto pre = gemm16_prefetch<12, KB32_D>(L16 + O16_FC1, wave, lane);
+                const auto pre = gemm16_prefetch<G16, 12, KB32_D>(L16 + O16_FC1, wave, lane);
                 const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
                 if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
                 BAR();
-                if (DPK_RUN(2)) graph_mma<false, true>(gf, B1, B2, nullptr, wave, lane);
+                if (DPK_RUN(2)) graph_mma<false, G16>(gf, B1, B2, nullptr, wave, lane);
                 BAR();
                 if (DPK_RUN(16 | 128)) {
                     const EpiArgs e{B2 + D, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg16<12, KB32_D, E_STORE_RELU, true>(B2b, LD2 * 4, L16 + O16_FC1, wave, lane, e, pre);
+                    gemm_wg16<G16, 12, KB32_D, E_STORE_RELU, G16>(B2b, LD2 * 4, L16 + O16_FC1, wave, lane, e, pre);
                 }
             } else {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
@@ -1790,10 +1827,10 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             {
                 const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<6, KB32_D2>(L16 + O16_FC2, wave, lane);
+                    const auto pre = gemm16_prefetch<G16, 6, KB32_D2>(L16 + O16_FC2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 256))
-                        gemm_wg16<6, KB32_D2, E_STORE_NB, false>(B2b + D * 4, LD2 * 4, L16 + O16_FC2, wave, lane, e, pre);
+                        gemm_wg16<G16, 6, KB32_D2, E_STORE_NB, 0>(B2b + D * 4, LD2 * 4, L16 + O16_FC2, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
                     BAR();
@@ -1804,14 +1841,14 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
                 const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
                 if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C1, wave, lane);
+                    const auto pre = gemm16_prefetch<G16, 6, KB32_D3>(L16 + O16_C1, wave, lane);
                     BAR();
                     if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
                     // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj));
                     //      cheb_prep reads only its own wave's rows of XS (wave = pose): no barrier
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, XS, B2, wave, lane);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, G16>(CW, XS, B2, wave, lane);
                     BAR();
-                    if (DPK_RUN(16 | 512)) gemm_wg16<6, KB32_D3, E_CHEB1, false>(B2b, LD2 * 4, L16 + O16_C1, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 512)) gemm_wg16<G16, 6, KB32_D3, E_CHEB1, 0>(B2b, LD2 * 4, L16 + O16_C1, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
                     BAR();
@@ -1824,12 +1861,12 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             {
                 const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<6, KB32_D3>(L16 + O16_C2, wave, lane);
+                    const auto pre = gemm16_prefetch<G16, 6, KB32_D3>(L16 + O16_C2, wave, lane);
                     BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, true>(CW, B1, B2, wave, lane);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, G16>(CW, B1, B2, wave, lane);
                     BAR();
                     if (DPK_RUN(16 | 1024))
-                        gemm_wg16<6, KB32_D3, E_RESID_RELU, false>(B2b, LD2 * 4, L16 + O16_C2, wave, lane, e, pre);
+                        gemm_wg16<G16, 6, KB32_D3, E_RESID_RELU, 0>(B2b, LD2 * 4, L16 + O16_C2, wave, lane, e, pre);
                 } else {
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
                     BAR();
@@ -1985,7 +2022,9 @@ struct dpk_handle {
     std::vector<float> h_arena;    // host staging of the arena
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
-    int gemm_mode = 0;             // 0: fp32 MFMA, 1: 3x fp16-split MFMA (dpk_set_gemm_mode)
+    char* arenabf = nullptr;       // device: bf16 GEMM weights (gemm mode 2), same layout
+    std::vector<uint16_t> h_arenabf;
+    int gemm_mode = 0;             // 0: fp32 MFMA, 1: 3x fp16-split MFMA, 2: bf16 MFMA (dpk_set_gemm_mode)
     bool w16_ok = true;            // loaded weights fit the split-fp16 packing (|w| < 1015)
     std::vector<float> h_temb;
     bool have_graph = false, have_weights = false, have_sched = false;
@@ -2046,9 +2085,18 @@ static void pack_blocks(float* dst, int Kreal, int Nreal, int KB, int NC, F w) {
                 }
 }
 
-// Split W_eff * W16_SCALE into fp16 hi + lo 16x16x32 B fragments [NC][KB32][hi|lo][64][8].
-// hi = fp16(v) (RNE), lo = fp16(v - hi); v - hi is exact in fp32 (Sterbenz).
-template <class F>
+// Host fp32 -> bf16, round to nearest even (finite inputs).
+static inline uint16_t bf16_rne(float v) {
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+static inline float bf16_to_f32(uint16_t b) { return __builtin_bit_cast(float, (uint32_t)b << 16); }
+
+// Split W_eff * W16_SCALE into hi + lo 16x16x32 B fragments [NC][KB32][hi|lo][64][8]:
+// BF = false: hi = fp16(v) (RNE), lo = fp16(v - hi); v - hi is exact in fp32 (Sterbenz).
+// BF = true:  the same with bf16 (gemm mode 2 reads only hi).
+template <bool BF = false, class F>
 static float pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
     float wmax = 0.f;
     for (int ct = 0; ct < NC; ++ct)
@@ -2059,11 +2107,19 @@ static float pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) 
                     const int n = ct * 16 + (lane & 15);
                     const float v = (k < Kreal && n < Nreal) ? w(k, n) * W16_SCALE : 0.f;
                     wmax = fmaxf(wmax, fabsf(v));
-                    const _Float16 hi = (_Float16)v;
-                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    uint16_t hb, lb;
+                    if constexpr (BF) {
+                        hb = bf16_rne(v);
+                        lb = bf16_rne(v - bf16_to_f32(hb));
+                    } else {
+                        const _Float16 hi = (_Float16)v;
+                        const _Float16 lo = (_Float16)(v - (float)hi);
+                        hb = __builtin_bit_cast(uint16_t, hi);
+                        lb = __builtin_bit_cast(uint16_t, lo);
+                    }
                     const size_t base = ((size_t)(ct * KB32 + kb) * BLK16) / 2;
-                    dst[base + lane * 8 + i] = __builtin_bit_cast(uint16_t, hi);
-                    dst[base + 512 + lane * 8 + i] = __builtin_bit_cast(uint16_t, lo);
+                    dst[base + lane * 8 + i] = hb;
+                    dst[base + 512 + lane * 8 + i] = lb;
                 }
     return wmax;
 }
@@ -2119,6 +2175,8 @@ static int upload(dpk_handle* h) {
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
     if (!h->arena16) HIPCHK(h, hipMalloc(&h->arena16, (size_t)ARENA16_BYTES));
     HIPCHK(h, hipMemcpy(h->arena16, h->h_arena16.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
+    if (!h->arenabf) HIPCHK(h, hipMalloc(&h->arenabf, (size_t)ARENA16_BYTES));
+    HIPCHK(h, hipMemcpy(h->arenabf, h->h_arenabf.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
     if (!h->temb) HIPCHK(h, hipMalloc(&h->temb, (size_t)TEMB_FLOATS * 4));
     HIPCHK(h, hipMemcpy(h->arena, h->h_arena.data(), (size_t)ARENA_FLOATS * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->temb, h->h_temb.data(), (size_t)TEMB_FLOATS * 4, hipMemcpyHostToDevice));
@@ -2128,13 +2186,16 @@ static int upload(dpk_handle* h) {
 // the sampler kernel for the handle's graph pattern and GEMM mode
 template <int MODE>
 static void launch_sampler(dpk_handle* h, dim3 grid, hipStream_t st, const SampleArgs& a) {
-    const bool g16 = h->gemm_mode == 1;
+    const int gm = h->gemm_mode;
+    const char* a16 = gm == 2 ? h->arenabf : h->arena16;
     if (h->sparse_graph) {
-        if (g16) hipLaunchKernelGGL((sample_kernel<MODE, true, true>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
-        else hipLaunchKernelGGL((sample_kernel<MODE, true, false>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+        if (gm == 1) hipLaunchKernelGGL((sample_kernel<MODE, true, 1>), grid, dim3(NT), 0, st, a, h->arena, a16);
+        else if (gm == 2) hipLaunchKernelGGL((sample_kernel<MODE, true, 2>), grid, dim3(NT), 0, st, a, h->arena, a16);
+        else hipLaunchKernelGGL((sample_kernel<MODE, true, 0>), grid, dim3(NT), 0, st, a, h->arena, a16);
     } else {
-        if (g16) hipLaunchKernelGGL((sample_kernel<MODE, false, true>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
-        else hipLaunchKernelGGL((sample_kernel<MODE, false, false>), grid, dim3(NT), 0, st, a, h->arena, h->arena16);
+        if (gm == 1) hipLaunchKernelGGL((sample_kernel<MODE, false, 1>), grid, dim3(NT), 0, st, a, h->arena, a16);
+        else if (gm == 2) hipLaunchKernelGGL((sample_kernel<MODE, false, 2>), grid, dim3(NT), 0, st, a, h->arena, a16);
+        else hipLaunchKernelGGL((sample_kernel<MODE, false, 0>), grid, dim3(NT), 0, st, a, h->arena, a16);
     }
 }
 
@@ -2167,6 +2228,7 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     else h->phase_delay = WG_PER_CU == 2 ? 60000 : 0;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_arena16.assign(ARENA16_BYTES / 2, 0);
+    h->h_arenabf.assign(ARENA16_BYTES / 2, 0);
     h->h_temb.assign(TEMB_FLOATS, 0.f);
     *out = h;
     return DPK_OK;
@@ -2177,6 +2239,7 @@ void dpk_destroy(dpk_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->arena) (void)hipFree(h->arena);
     if (h->arena16) (void)hipFree(h->arena16);
+    if (h->arenabf) (void)hipFree(h->arenabf);
     if (h->temb) (void)hipFree(h->temb);
     if (h->coef) (void)hipFree(h->coef);
     if (h->tproj) (void)hipFree(h->tproj);
@@ -2313,6 +2376,16 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         w16max = fmaxf(w16max, pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; }));
         w16max = fmaxf(w16max, pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; }));
         w16max = fmaxf(w16max, pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; }));
+        uint16_t* Lb = h->h_arenabf.data() + (size_t)l * LAYER16_BYTES / 2;
+        (void)(pack16<true>(Lb + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
+            const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
+            return w[(n % D) * D + k];
+        }));
+        (void)(pack16<true>(Lb + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; }));
+        (void)(pack16<true>(Lb + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; }));
+        (void)(pack16<true>(Lb + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; }));
+        (void)(pack16<true>(Lb + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; }));
+        (void)(pack16<true>(Lb + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; }));
         for (int c = 0; c < D; ++c) {
             Lw[OFF_BQKV + c] = bq[c];
             Lw[OFF_BQKV + D + c] = bk[c];
@@ -2548,7 +2621,8 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
 
 int dpk_set_gemm_mode(dpk_handle* h, int mode) {
     if (!h) return DPK_E_INVALID;
-    if (mode != 0 && mode != 1) return fail(h, DPK_E_INVALID, "dpk_set_gemm_mode: mode must be 0 (fp32) or 1 (3xfp16)");
+    if (mode < 0 || mode > 2)
+        return fail(h, DPK_E_INVALID, "dpk_set_gemm_mode: mode must be 0 (fp32), 1 (3xfp16) or 2 (bf16)");
     h->gemm_mode = mode;
     return DPK_OK;
 }

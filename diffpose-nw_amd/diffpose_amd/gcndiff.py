@@ -147,11 +147,12 @@ class _HipModel:
             raise ValueError(f"x on {x.device}, model on {self.device}")
         return x.contiguous()
 
-    GEMM_MODES = {"fp32": 0, "f16x3": 1}
+    GEMM_MODES = {"fp32": 0, "f16x3": 1, "bf16": 2}
 
     def set_gemm_mode(self, mode: str = "fp32") -> None:
         """Arithmetic of the per-layer GEMMs (see dpk_set_gemm_mode): "fp32" (default, fp32 MFMA)
-        or "f16x3" (3-term fp16-split MFMA, fp32 accumulate).  Not a reference option: the
+        "f16x3" (3-term fp16-split MFMA, fp32 accumulate) or "bf16" (bf16 operands, fp32
+        accumulate: reduced precision, for the tolerance study).  Not a reference option: the
         reference runs fp32 throughout, and "fp32" is what its parity is pinned on."""
         if mode not in self.GEMM_MODES:
             raise ValueError(f"gemm mode must be one of {sorted(self.GEMM_MODES)}, got {mode!r}")

@@ -153,8 +153,10 @@ int dpk_gmm_sample(const float* gmm_dev, const float* poses3d_dev, int n_src, in
  * interface; the reference computes everything in fp32 on its device):
  *   mode 0 (default): fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 accumulate;
  *   mode 1: 3-term fp16 split (a = a_hi + a_lo, w*64 = w_hi + w_lo; a_hi w_hi + a_hi w_lo +
- *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products.
- * The input/output ChebConvs, LayerNorm, attention and the DDIM update stay fp32 in both.
+ *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products;
+ *   mode 2: bf16 (a and w rounded to bf16, one v_mfma_f32_16x16x32_bf16 product, fp32
+ *           accumulate): a reduced-precision mode for the tolerance study of BASELINE config 3.
+ * The input/output ChebConvs, LayerNorm, attention and the DDIM update stay fp32 in all modes.
  * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle.  Range: mode 1 needs
  * every GEMM weight |w| < 1015 (else those calls return DPK_E_UNSUPPORTED) and GEMM inputs
  * (LayerNorm/attention/graph/Chebyshev outputs) below 65504 in magnitude; an overflow there

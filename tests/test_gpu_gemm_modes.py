@@ -153,7 +153,7 @@ def test_gcnpose_f16x3_vs_golden(golden):
 
 def test_bad_gemm_mode_raises(model):
     with pytest.raises(ValueError):
-        model.set_gemm_mode("bf16")
+        model.set_gemm_mode("tf32")
 
 
 def test_out_of_range_weights_are_refused():

@@ -1,0 +1,60 @@
+"""Instruction mix of one device function inside the sampler kernel (build container only).
+
+Inserts asm comment markers at the entry and the last closing brace of the named
+__device__ function, compiles the kernel source to gfx950 assembly and counts the
+instructions between the first pair of markers inside the chosen kernel instance.
+  python tools/isa_count.py layer_norm [--kernel _ZN3dpk13sample_kernelILi0ELb1ELb0EE]
+"""
+import argparse
+import collections
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_kernels.hip")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("func")
+    ap.add_argument("--kernel", default="_ZN3dpk13sample_kernelILi0ELb1ELb0EE")
+    ap.add_argument("--nth", type=int, default=0, help="which marked region inside the kernel")
+    a = ap.parse_args()
+    s = open(SRC).read()
+    i = s.index(f"__device__ __forceinline__ void {a.func}(")
+    b = s.index("{", i)
+    # matching closing brace
+    depth, j = 0, b
+    while True:
+        if s[j] == "{":
+            depth += 1
+        elif s[j] == "}":
+            depth -= 1
+            if depth == 0:
+                break
+        j += 1
+    body = s[b + 1:j]
+    s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN");' + body.replace("return;", 'asm volatile(";MARK_END"); return;') \
+        + '    asm volatile(";MARK_END");\n' + s[j:]
+    tmp = "/tmp/isa_count.hip"
+    open(tmp, "w").write(s2)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-fno-slp-vectorize", f"-I{ROOT}/include", "-Wno-unused-result", "--cuda-device-only", "-S",
+                    tmp, "-o", "/tmp/isa_count.s"], check=True, stderr=subprocess.DEVNULL)
+    asm = open("/tmp/isa_count.s").read()
+    k = asm.index(a.kernel)
+    k = asm.index(a.kernel + "EvNS_10SampleArgsEPKfPKc:", k) if (a.kernel + "EvNS_10SampleArgsEPKfPKc:") in asm else k
+    pos = k
+    for _ in range(a.nth + 1):
+        st = asm.index(";MARK_BEGIN", pos)
+        en = asm.index(";MARK_END", st)
+        pos = en
+    ins = [l.strip() for l in asm[st:en].splitlines()
+           if l.strip() and not l.strip().startswith((";", "."))]
+    c = collections.Counter(x.split()[0] for x in ins)
+    print(len(ins), "instructions")
+    print(c.most_common(40))
+
+
+if __name__ == "__main__":
+    main()

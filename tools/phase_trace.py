@@ -25,7 +25,7 @@ SO = os.path.join(ROOT, "build", "trace", "libdpk_trace.so")
 def _events(gemm_mode="fp32"):
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
-    npass = {"QKV": 3, "fc1": 2} if gemm_mode == "f16x3" else {}
+    npass = {"QKV": 3, "fc1": 2} if gemm_mode in ("f16x3", "bf16") else {}
 
     def gemm(n):
         for _ in range(npass.get(n.split(".")[-1], 1)):
@@ -118,7 +118,7 @@ if __name__ == "__main__":
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--step", type=int, default=10)
-    ap.add_argument("--gemm", choices=("fp32", "f16x3"), default="fp32")
+    ap.add_argument("--gemm", choices=("fp32", "f16x3", "bf16"), default="fp32")
     a = ap.parse_args()
     if a.build:
         build()
