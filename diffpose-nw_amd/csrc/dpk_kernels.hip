@@ -86,6 +86,9 @@ constexpr int PE = J * CIN;  // floats per pose (85)
 #ifndef DPK_ATTN_MMA
 #define DPK_ATTN_MMA 1       // attention on the matrix cores (attention_mma) or on DPP rows (attention)
 #endif
+#ifndef DPK_LN_FUSE
+#define DPK_LN_FUSE 0        // 1: fp32 mode: LayerNorm statistics from the producing GEMM epilogue, applied in the consumer
+#endif
 #ifndef DPK_P
 #define DPK_P 4              // poses per workgroup: 4 (one workgroup per CU) or 2 (two per CU)
 #endif
@@ -104,7 +107,9 @@ constexpr int SM_B1 = SM_XS + R * LDX;      // 96-wide scratch   [R][LDX]
 constexpr int SM_B2 = SM_B1 + R * LDX;      // 288-wide scratch  [R][LD2]
 constexpr int SM_XST = SM_B2 + R * LD2;     // pose state x_t    [R][5]
 constexpr int SM_LNP = SM_XST + ((R * CIN + 3) / 4) * 4;   // LayerNorm gains/shifts of all layers [NL][4][D]
-constexpr int SM_FLOATS = SM_LNP + NL * 4 * D;
+constexpr int SM_ST = SM_LNP + NL * 4 * D;                  // LayerNorm row statistics (fused LN, below)
+constexpr int ST_TAIL = 64 * 4;                             // [64 main rows][mean0, M2_0, mean1, M2_1]
+constexpr int SM_FLOATS = SM_ST + ST_TAIL + 4 * 4 * 4;      // + [4 tail rows][4 waves][n, mean, M2, -]
 static_assert(SM_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
 // packed-weight blocks: one block = 16 cols x 16 k = 64 lanes x float4
@@ -285,6 +290,13 @@ __device__ __forceinline__ float normal_noise(unsigned long long seed, int step,
 __device__ __forceinline__ void ddim_elem(const float* cf, float xt, float et, float z, float& x0, float& xn) {
     x0 = (xt - et * cf[0]) / cf[1];
     xn = (cf[2] * x0 + cf[3] * z) + cf[4] * et;
+}
+
+// DPP row (16-lane) rotations and all-reduces
+template <int J>
+__device__ __forceinline__ float row_ror(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
+                                                                 0x120 + J, 0xf, 0xf, false));
 }
 
 // Sum over the 4 lane rows (l, l^16, l^32, l^48), result in every lane, on the VALU: a
@@ -480,7 +492,57 @@ struct EpiArgs {
     int tproj_pose_stride;  // 0: one row for all poses; else floats between consecutive poses
     int pose0;              // global index of the workgroup's first pose (eps mode clamp)
     int pose_max;           // N-1
+    float* st = nullptr;    // STATS epilogues: LayerNorm partial statistics of the rows written (LDS)
 };
+
+// ---- fused LayerNorm (fp32 GEMM mode, DPK_LN_FUSE) ------------------------------------------
+// GraFormer's LayerNorm (GraFormer.py:58-70) is split across the phases around it: the GEMM
+// epilogue that writes the residual stream x (gconv_input, O-proj, Cheb2) also reduces, per
+// row and per 48-column half it owns, (mean, M2 = sum (x - mean)^2) over its final values (rows
+// 64..67: per wave, (n, mean, M2) over the tail columns it owns), into LDS; the consumer (the QKV
+// GEMM's A-operand ring for LN0, the GraphNet product for LN1) merges the partials with Chan et
+// al.'s pairwise update and applies a*(x-mean)/(std+eps)+b to its operand registers, so the LN
+// phase, its LDS round trip and its barrier disappear.  std is the unbiased (/95) one.
+// merge partial b into a: f = n_b / (n_a + n_b), g = n_a n_b / (n_a + n_b)
+__device__ __forceinline__ void chan_merge(float& m, float& M2, float mb, float M2b, float f, float g) {
+    const float d = mb - m;
+    m = fmaf(d, f, m);
+    M2 = (M2 + M2b) + (d * d) * g;
+}
+// 1/d to ~0.5 ulp: v_rcp_f32 plus one Newton step
+__device__ __forceinline__ float rcp_nr(float d) {
+    const float r = __builtin_amdgcn_rcpf(d);
+    return fmaf(r, fmaf(-d, r, 1.0f), r);
+}
+// (mean, 1/(std + eps)) of workgroup row `row` from the partials in st
+__device__ __forceinline__ f32x2 ln_row_norm(const float* st, int row) {
+    constexpr int RM = R - R % 16;
+    float m, M2;
+    if (row < RM) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(st + row * 4);
+        const float d = v[2] - v[0];
+        m = (v[0] + v[2]) * 0.5f;
+        M2 = (v[1] + v[3]) + (d * d) * 24.0f;            // n_a n_b / (n_a + n_b) = 48*48/96
+    } else {
+        // tail columns per wave (gemm_wave, N = 96): waves 0,1 own 32, waves 2,3 own 16
+        static_assert(R == 68, "tail partial counts");
+        const float* t = st + ST_TAIL + (row - RM) * 16;
+        const f32x4 p0 = *reinterpret_cast<const f32x4*>(t), p1 = *reinterpret_cast<const f32x4*>(t + 4);
+        const f32x4 p2 = *reinterpret_cast<const f32x4*>(t + 8), p3 = *reinterpret_cast<const f32x4*>(t + 12);
+        m = p0[1];
+        M2 = p0[2];
+        chan_merge(m, M2, p1[1], p1[2], 0.5f, 16.0f);                    // 32 + 32
+        chan_merge(m, M2, p2[1], p2[2], 0.2f, 12.8f);                    // 64 + 16
+        chan_merge(m, M2, p3[1], p3[2], 1.0f / 6.0f, 80.0f / 6.0f);      // 80 + 16
+    }
+    constexpr float RD1 = 1.0f / (float)(D - 1);
+    const float den = __builtin_amdgcn_sqrtf(M2 * RD1) + LN_EPS;   // v_sqrt_f32 (1 ulp)
+    return f32x2{m, rcp_nr(den)};
+}
+// a*(x-mean)/(std+eps)+b on 4 consecutive columns of one row
+__device__ __forceinline__ f32x4 ln_apply4(f32x4 x, f32x2 nrm, f32x4 gain, f32x4 shift) {
+    return __builtin_elementwise_fma((x - nrm[0]) * nrm[1], gain, shift);
+}
 
 template <int MODE>
 __device__ __forceinline__ float epi_value(float acc, float bias, float tp, float old) {
@@ -503,10 +565,14 @@ __device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, fl
 // One wave: row tiles [rt0, rt0+NR) on MFMA plus the tail (TM) over NCW column tiles from ct0,
 // visited in rotated order (local tile c = global ct0 + (c + rot) mod NCW); 2-stage register
 // ring (named buffers, loop unrolled by 2, last pair peeled).
-template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE>
+// STATS: the epilogue also writes the fused-LayerNorm partials of its rows (N = 96 only);
+// LNA: the A operand is raw x, normalised in registers with the statistics in `lst` and the
+// gains/shifts lg/lb (LDS) before it feeds the MFMAs (fused LayerNorm, see ln_row_norm).
+template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE, bool STATS = false, bool LNA = false>
 __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* Bp, int rt0, int ct0, int rot,
                                           int trow0, bool tail_dup, int lane, const EpiArgs& e,
-                                          const BPre<NCW>& pre) {
+                                          const BPre<NCW>& pre, const float* lst = nullptr,
+                                          const float* lg = nullptr, const float* lb = nullptr) {
     using T = GemmTile<NR, NCW, TM, TR, KB>;
     constexpr int TA = T::TA, NQ = T::NQ;
     static_assert(KB == 1 || KB % 2 == 0, "k-blocks in pairs");
@@ -569,6 +635,36 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     constexpr int S = (KB == 1) ? 1 : (NCW <= 6 && KB % 3 == 0) ? 3 : 2;
     static_assert(KB == 1 || KB % S == 0, "ring slots divide the k-blocks");
     f32x4 as[S][NR], ts[S][TA], bs[S][NCW];
+    f32x4 gs[S], ss[S];                         // LNA: gains / shifts of the slot's k's
+    f32x2 nrm[NR], tnrm = {0.f, 0.f};           // LNA: (mean, 1/(std+eps)) of the lane's rows
+    if constexpr (LNA) {
+        static_assert(TM == TM_MFMA4, "fused LN operand: 4x4x1 tail rows");
+#pragma unroll
+        for (int i = 0; i < NR; ++i) nrm[i] = ln_row_norm(lst, (rt0 + i) * 16 + rl);
+        tnrm = ln_row_norm(lst, trow0 + (lane & 3));
+    }
+    auto loadLN = [&](int st, int kb) {
+        if constexpr (LNA) {
+            gs[st] = *reinterpret_cast<const f32x4*>(lg + kb * 16 + kq);
+            ss[st] = *reinterpret_cast<const f32x4*>(lb + kb * 16 + kq);
+        }
+    };
+    // LNA: slot st's operand is normalised one ring block ahead, between the previous slot's
+    // MFMAs (scalar VALU fills their issue gaps; packed f32 ops beside MFMAs cost more)
+    auto lnx = [&](int st) {
+        if constexpr (LNA) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                for (int i = 0; i < NR; ++i) as[st][i][j] = fmaf((as[st][i][j] - nrm[i][0]) * nrm[i][1], gs[st][j], ss[st][j]);
+                ts[st][0][j] = fmaf((ts[st][0][j] - tnrm[0]) * tnrm[1], gs[st][j], ss[st][j]);
+            }
+        }
+    };
+    auto mma = [&](int st) {
+        g.mma(as[st], ts[st], bs[st]);
+        if constexpr (LNA) lnx(st + 1 < S ? st + 1 : 0);
+    };
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
         bs[0][c] = pre.b0[c];
@@ -578,21 +674,29 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
 #pragma unroll
     for (int st = 2; st < S; ++st) T::loadB(bs[st], src, soff, st);
 #pragma unroll
-    for (int st = 0; st < S; ++st) g.loadA(as[st], ts[st], A, st);
+    for (int st = 0; st < S; ++st) {
+        g.loadA(as[st], ts[st], A, st);
+        loadLN(st, st);
+    }
+    lnx(0);
     if constexpr (KB > S) {
 #pragma unroll 1
         for (int kb = 0; kb < KB - S; kb += S) {
 #pragma unroll
             for (int st = 0; st < S; ++st) {
-                g.mma(as[st], ts[st], bs[st]);
+                mma(st);
                 T::loadB(bs[st], src, soff, kb + st + S);
                 g.loadA(as[st], ts[st], A, kb + st + S);
+                loadLN(st, kb + st + S);
                 T::schedule_half();
             }
         }
     }
 #pragma unroll
-    for (int st = 0; st < S; ++st) g.mma(as[st], ts[st], bs[st]);
+    for (int st = 0; st < S; ++st) {
+        g.mma(as[st], ts[st], bs[st]);
+        if (st + 1 < S) lnx(st + 1);
+    }
     DPK_GEMM_HOOK(1);
     constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
     auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
@@ -612,6 +716,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
         const int row = (rt0 + i) * 16 + rl;
+        f32x4 vo[NCW];
 #pragma unroll
         for (int c = 0; c < NCW; ++c) {
             const int col4 = gcol[c] * 16 + kq;
@@ -621,6 +726,21 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
             for (int r = 0; r < 4; ++r)
                 v[r] = epi_value<MODE>(g.acc[i][c][r], bias4[c][r], tp[r], RES ? old[i][c][r] : 0.f);
             *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
+            vo[c] = v;
+        }
+        if constexpr (STATS) {
+            // this row's 48 columns of the half: 12 in this lane, the rest in lanes l^16, l^32, l^48
+            static_assert(NCW == 3, "LayerNorm partials over 48-column halves");
+            const f32x4 s4 = (vo[0] + vo[1]) + vo[2];
+            const float mh = sum4rows((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.0f / 48.0f);
+            f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < NCW; ++c) {
+                const f32x4 d = vo[c] - mh;
+                q4 = __builtin_elementwise_fma(d, d, q4);
+            }
+            const float m2 = sum4rows((q4[0] + q4[1]) + (q4[2] + q4[3]));
+            if (lane < 16) *reinterpret_cast<f32x2*>(e.st + row * 4 + 2 * (ct0 / NCW)) = f32x2{mh, m2};
         }
     }
     if constexpr (TM == TM_VALU) {
@@ -628,15 +748,41 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     } else if constexpr (TM == TM_MFMA4) {
         // reduce-scatter the 4 k-slices: lane l then holds tail row l&3, column tcol of tile q
         const int row = trow0 + (lane & 3);
+        float tv[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const float v = rs4rows(g.tacc[q][0], g.tacc[q][1], g.tacc[q][2], g.tacc[q][3]);
+            tv[q] = 0.f;
             if ((q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
             const int col = gcol[q] * 16 + tcol;
             float* dp = e.dst + row * e.ldd + col;
             const float oldt = RES ? *dp : 0.f;
             const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
-            *dp = epi_value<MODE>(v, tbias[q], tp, oldt);
+            tv[q] = epi_value<MODE>(v, tbias[q], tp, oldt);
+            *dp = tv[q];
+        }
+        if constexpr (STATS) {
+            // tail row l&3: this wave's valid tail tiles, 16 columns each, spread over the 16 lanes
+            // with that l&3 (lane bits 2-3 by DPP row rotation, bits 4-5 by permlane)
+            const int nq = (NQ - (tail_dup ? 1 : 0));
+            const float cnt = 16.0f * (float)nq;   // 32 (waves 0,1) or 16 (waves 2,3)
+            float sm = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) sm += (q < nq) ? tv[q] : 0.f;
+            sm += row_ror<4>(sm);
+            sm += row_ror<8>(sm);
+            const float mt = sum4rows(sm) * (1.0f / 16.0f) * (nq == 2 ? 0.5f : 1.0f);
+            float sq = 0.f;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float d = tv[q] - mt;
+                sq += (q < nq) ? d * d : 0.f;
+            }
+            sq += row_ror<4>(sq);
+            sq += row_ror<8>(sq);
+            sq = sum4rows(sq);
+            const int wv = 2 * (rt0 / NR) + (ct0 / NCW);   // wave index (row pair, column half)
+            if (lane < 4 && row < R) *reinterpret_cast<f32x4*>(e.st + ST_TAIL + (lane * 4 + wv) * 4) = f32x4{cnt, mt, sq, 0.f};
         }
     }
     DPK_GEMM_HOOK(2);
@@ -645,16 +791,18 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
 // Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
 // 2*(w>>1)+1 and column half w&1 on the 16x16x4 MFMA; the 4 tail rows 64..67 of that column
 // half on 4x4x1 MFMAs, split between the half's two waves (rotated column order for w>>1 = 1).
-template <int NC, int KB, int MODE>
+template <int NC, int KB, int MODE, bool STATS = false, bool LNA = false>
 __device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp, int wave, int lane,
-                                        const EpiArgs& e, const BPre<NC / 2>& pre) {
+                                        const EpiArgs& e, const BPre<NC / 2>& pre, const float* lst = nullptr,
+                                        const float* lg = nullptr, const float* lb = nullptr) {
     static_assert(NC % 2 == 0 && (R == 68 || R == 34) && NW == 4, "row tiles x 2 column halves + tail rows");
     constexpr int NCW = NC / 2;
     constexpr int NRW = R == 68 ? 2 : 1;            // row tiles per wave
     const int pr = gemm_pr(wave);
     const bool dup = (NCW & 1) && pr == 1;
-    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW, col_rot<NCW>(wave),
-                                                   R - R % 16, dup, lane, e, pre);
+    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE, STATS, LNA>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW,
+                                                               col_rot<NCW>(wave), R - R % 16, dup, lane, e, pre,
+                                                               lst, lg, lb);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -966,12 +1114,7 @@ __device__ __forceinline__ float div_by(float x, float d, float r) {
     return fmaf(e, r, q);
 }
 
-// DPP row (16-lane) rotations and all-reduces
-template <int J>
-__device__ __forceinline__ float row_ror(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
-                                                                 0x120 + J, 0xf, 0xf, false));
-}
+// DPP row (16-lane) all-reduces (row_ror: before sum4rows)
 // all-reduce over the 16 lanes of a DPP row
 __device__ __forceinline__ float row_max(float v) {
     v = fmaxf(v, row_ror<8>(v));
@@ -1577,9 +1720,13 @@ __device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int la
     return f;
 }
 
-template <bool RESID, int SPLIT_OUT = 0>
+// LNA: src is raw x; the operand is LayerNorm(x) formed in registers (fused LN1: statistics
+// from the O-proj epilogue in lst, gains/shifts ng/nb in LDS; see ln_row_norm).
+template <bool RESID, int SPLIT_OUT = 0, bool LNA = false>
 __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, float* dst,
-                                          const float* __restrict__ bias, int wave, int lane) {
+                                          const float* __restrict__ bias, int wave, int lane,
+                                          const float* lst = nullptr, const float* ng = nullptr,
+                                          const float* nb = nullptr) {
     lane = opaque(lane);
     if (wave >= P) return;
     const int g = lane >> 4, cl = lane & 15;
@@ -1592,6 +1739,20 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
         const int row = min(4 * s + g, J - 1);
 #pragma unroll
         for (int t = 0; t < 6; ++t) a[t][s] = xp[row * LDX + 16 * t];
+    }
+    if constexpr (LNA) {
+        float gn[6], sh[6];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            gn[t] = ng[16 * t + cl];
+            sh[t] = nb[16 * t + cl];
+        }
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+            const f32x2 nrm = ln_row_norm(lst, wave * J + min(4 * s + g, J - 1));
+#pragma unroll
+            for (int t = 0; t < 6; ++t) a[t][s] = fmaf((a[t][s] - nrm[0]) * nrm[1], gn[t], sh[t]);
+        }
     }
     f32x4 acc[6];
     float p16[6];
@@ -1688,6 +1849,8 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
     float* B2 = sm + SM_B2;
     float* XST = sm + SM_XST;
     float* LNP = sm + SM_LNP;
+    float* ST = sm + SM_ST;
+    constexpr bool LNF = DPK_LN_FUSE && G16 == 0 && R == 68;   // fused LayerNorm (fp32 GEMM mode)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
@@ -1743,13 +1906,17 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
 #endif
 #pragma unroll 1
     for (int s = 0; s < K; ++s) {
+        // LNF: QKV's first B k-blocks are in flight a whole GEMM ahead (the LN phase that used to
+        // cover their L2 latency is gone): layer 0's here, layer l+1's before layer l's Cheb2 GEMM
+        BPre<9> qpre;
+        if constexpr (LNF) qpre = gemm_prefetch<18, 6>(W + OFF_QKV, wave, lane);
         // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
         {
             const auto pre = gemm_prefetch<6, 1>(W + OFF_WIN, wave, lane);
             input_prep<SPARSE>(CW, XST, B1, tid);
             BAR();
-            const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1};
-            gemm_wg<6, 1, E_STORE>(B1, LDX, W + OFF_WIN, wave, lane, e, pre);
+            const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1, ST};
+            gemm_wg<6, 1, E_STORE, LNF>(B1, LDX, W + OFF_WIN, wave, lane, e, pre);
         }
         BAR();
 
@@ -1767,6 +1934,11 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     if (DPK_RUN(8)) layer_norm<G16>(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
                     BAR();
                     if (DPK_RUN(16 | 32)) gemm_wg16<G16, 18, KB32_D, E_STORE, 0>(B1b, LDX * 4, L16 + O16_QKV, wave, lane, e, pre);
+                } else if constexpr (LNF) {
+                    // LN0 fused: QKV reads x and normalises its A operand (partials from Cheb2 / gconv_input)
+                    if (DPK_RUN(16 | 32))
+                        gemm_wg<18, 6, E_STORE, false, true>(XS, LDX, LW + OFF_QKV, wave, lane, e, qpre, ST,
+                                                             LNP + l * 4 * D, LNP + l * 4 * D + D);
                 } else {
                     const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
                     if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
@@ -1776,7 +1948,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             }
             BAR();
             {
-                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1};
+                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1, ST};
                 if constexpr (G16) {
                     const auto pre = gemm16_prefetch<G16, 6, KB32_D>(L16 + O16_O, wave, lane);
                     if (DPK_RUN(1)) {
@@ -1792,7 +1964,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                         else attention(B2, B1, a.mask, tid);
                     }
                     BAR();
-                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID, LNF>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
                 }
             }
             BAR();
@@ -1814,9 +1986,16 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             } else {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
                 const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
-                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
-                BAR();
-                if (DPK_RUN(2)) graph_mma<false>(gf, B1, B1, nullptr, wave, lane);
+                if constexpr (LNF) {
+                    // LN1 fused into the GraphNet product's operand (partials from the O-proj epilogue)
+                    if (DPK_RUN(2))
+                        graph_mma<false, 0, true>(gf, XS, B1, nullptr, wave, lane, ST, LNP + l * 4 * D + 2 * D,
+                                                  LNP + l * 4 * D + 3 * D);
+                } else {
+                    if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
+                    BAR();
+                    if (DPK_RUN(2)) graph_mma<false>(gf, B1, B1, nullptr, wave, lane);
+                }
                 BAR();
                 if (DPK_RUN(16 | 128)) {
                     const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
@@ -1859,7 +2038,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 }
             }
             {
-                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1};
+                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1, ST};
                 if constexpr (G16) {
                     const auto pre = gemm16_prefetch<G16, 6, KB32_D3>(L16 + O16_C2, wave, lane);
                     BAR();
@@ -1872,7 +2051,9 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     BAR();
                     if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, wave, lane);
                     BAR();
-                    if (DPK_RUN(16 | 1024)) gemm_wg<6, 18, E_RESID_RELU>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
+                    if constexpr (LNF)
+                        if (l + 1 < NL) qpre = gemm_prefetch<18, 6>(LW + LAYER_FLOATS + OFF_QKV, wave, lane);
+                    if (DPK_RUN(16 | 1024)) gemm_wg<6, 18, E_RESID_RELU, LNF>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
                 }
             }
             BAR();

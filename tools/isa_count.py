@@ -17,7 +17,7 @@ SRC = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_kernels.hip")
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("func")
-    ap.add_argument("--kernel", default="_ZN3dpk13sample_kernelILi0ELb1ELb0EE")
+    ap.add_argument("--kernel", default="_ZN3dpk13sample_kernelILi0ELb1ELi0EE")
     ap.add_argument("--nth", type=int, default=0, help="which marked region inside the kernel")
     a = ap.parse_args()
     s = open(SRC).read()
@@ -34,8 +34,8 @@ def main():
                 break
         j += 1
     body = s[b + 1:j]
-    s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN");' + body.replace("return;", 'asm volatile(";MARK_END"); return;') \
-        + '    asm volatile(";MARK_END");\n' + s[j:]
+    s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN" ::: "memory");' + body.replace("return;", 'asm volatile(";MARK_END" ::: "memory"); return;') \
+        + '    asm volatile(";MARK_END" ::: "memory");\n' + s[j:]
     tmp = "/tmp/isa_count.hip"
     open(tmp, "w").write(s2)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
@@ -47,7 +47,10 @@ def main():
     pos = k
     for _ in range(a.nth + 1):
         st = asm.index(";MARK_BEGIN", pos)
-        en = asm.index(";MARK_END", st)
+        nxt = asm.find(";MARK_BEGIN", st + 1)
+        if nxt < 0:
+            nxt = len(asm)
+        en = asm.rindex(";MARK_END", st, nxt)      # the last exit of this inlined copy
         pos = en
     ins = [l.strip() for l in asm[st:en].splitlines()
            if l.strip() and not l.strip().startswith((";", "."))]

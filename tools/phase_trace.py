@@ -22,7 +22,10 @@ SO = os.path.join(ROOT, "build", "trace", "libdpk_trace.so")
 # stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
 # ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
 # the split-fp16 GEMMs (gemm mode f16x3) run a wave's column tiles in passes of 3 and stamp per pass
-def _events(gemm_mode="fp32"):
+def _events(gemm_mode="fp32", fused=None):
+    # fp32 mode built with -DDPK_LN_FUSE=1: no LayerNorm phases (LN0 in the QKV operand, LN1 in graph1)
+    if fused is None:
+        fused = gemm_mode == "fp32" and os.environ.get("DPK_LN_FUSE", "0") == "1"
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
     npass = {"QKV": 3, "fc1": 2} if gemm_mode in ("f16x3", "bf16") else {}
@@ -33,9 +36,13 @@ def _events(gemm_mode="fp32"):
     bar("input_prep"); gemm("input_gemm"); bar("input_gemm")
     for l in range(5):
         p = f"L{l}."
-        bar(p + "LN0"); gemm(p + "QKV"); bar(p + "QKV")
+        if not fused:
+            bar(p + "LN0")
+        gemm(p + "QKV"); bar(p + "QKV")
         bar(p + "attention"); gemm(p + "O"); bar(p + "O")
-        bar(p + "LN1"); bar(p + "graph1"); gemm(p + "fc1"); bar(p + "fc1")
+        if not fused:
+            bar(p + "LN1")
+        bar(p + ("LN1+graph1" if fused else "graph1")); gemm(p + "fc1"); bar(p + "fc1")
         gemm(p + "fc2"); bar(p + "fc2")
         bar(p + "graph2+cheb1"); gemm(p + "C1"); bar(p + "C1")
         bar(p + "cheb_prep2"); gemm(p + "C2"); bar(p + "C2")
