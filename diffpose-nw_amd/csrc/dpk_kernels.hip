@@ -405,15 +405,21 @@ struct GemmTile {
         for (int c = 0; c < NCW; ++c)
             b[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c] + kb * 1024, 0));
     }
+    // FIRST: the GEMM's first k-step takes C = 0 as an inline constant (no accumulator zeroing:
+    // ~100 v_accvgpr_write per wave and GEMM otherwise)
+    template <bool FIRST = false>
     __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&t)[TA], const f32x4 (&b)[NCW]) {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
             for (int i = 0; i < NR; ++i)
 #pragma unroll
-                for (int c = 0; c < NCW; ++c)
-                    acc[i][c] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[c][j], a[i][j], acc[i][c], 0, 0, 0)
-                                      : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], acc[i][c], 0, 0, 0);
+                for (int c = 0; c < NCW; ++c) {
+                    const f32x4 cin = (FIRST && j == 0) ? z : acc[i][c];
+                    acc[i][c] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[c][j], a[i][j], cin, 0, 0, 0)
+                                      : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], cin, 0, 0, 0);
+                }
             if constexpr (TM == TM_VALU) {
 #pragma unroll
                 for (int c = 0; c < NCW; ++c)
@@ -421,7 +427,8 @@ struct GemmTile {
                     for (int r = 0; r < TR; ++r) tl[c][r] = fmaf(t[r][j], b[c][j], tl[c][r]);
             } else if constexpr (TM == TM_MFMA4) {
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(b[q][j], t[0][j], tacc[q], 0, 0, 0);
+                for (int q = 0; q < NQ; ++q)
+                    tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(b[q][j], t[0][j], (FIRST && j == 0) ? z : tacc[q], 0, 0, 0);
             }
         }
     }
@@ -577,17 +584,11 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     constexpr int TA = T::TA, NQ = T::NQ;
     static_assert(KB == 1 || KB % 2 == 0, "k-blocks in pairs");
     lane = opaque(lane);
-    T g;
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-        for (int c = 0; c < NCW; ++c) g.acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    T g;   // accumulators: set by the first k-step (mma<true>)
 #pragma unroll
     for (int c = 0; c < NCW; ++c)
 #pragma unroll
         for (int r = 0; r < TA; ++r) g.tl[c][r] = 0.f;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) g.tacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int rl = lane & 15, kq = (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < NR; ++i) g.aoff[i] = ((rt0 + i) * 16 + rl) * lda + kq;
@@ -665,6 +666,10 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         g.mma(as[st], ts[st], bs[st]);
         if constexpr (LNA) lnx(st + 1 < S ? st + 1 : 0);
     };
+    auto mma_first = [&]() {
+        g.template mma<true>(as[0], ts[0], bs[0]);
+        if constexpr (LNA) lnx(S > 1 ? 1 : 0);
+    };
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
         bs[0][c] = pre.b0[c];
@@ -680,8 +685,18 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     }
     lnx(0);
     if constexpr (KB > S) {
+        // first ring pass peeled: its k-step 0 starts the accumulators from C = 0
+#pragma unroll
+        for (int st = 0; st < S; ++st) {
+            if (st == 0) mma_first();
+            else mma(st);
+            T::loadB(bs[st], src, soff, st + S);
+            g.loadA(as[st], ts[st], A, st + S);
+            loadLN(st, st + S);
+            T::schedule_half();
+        }
 #pragma unroll 1
-        for (int kb = 0; kb < KB - S; kb += S) {
+        for (int kb = S; kb < KB - S; kb += S) {
 #pragma unroll
             for (int st = 0; st < S; ++st) {
                 mma(st);
@@ -691,11 +706,18 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
                 T::schedule_half();
             }
         }
-    }
 #pragma unroll
-    for (int st = 0; st < S; ++st) {
-        g.mma(as[st], ts[st], bs[st]);
-        if (st + 1 < S) lnx(st + 1);
+        for (int st = 0; st < S; ++st) {
+            g.mma(as[st], ts[st], bs[st]);
+            if (st + 1 < S) lnx(st + 1);
+        }
+    } else {
+#pragma unroll
+        for (int st = 0; st < S; ++st) {
+            if (st == 0) g.template mma<true>(as[st], ts[st], bs[st]);
+            else g.mma(as[st], ts[st], bs[st]);
+            if (st + 1 < S) lnx(st + 1);
+        }
     }
     DPK_GEMM_HOOK(1);
     constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
