@@ -2222,6 +2222,13 @@ struct dpk_handle {
     float* coef = nullptr;         // device: [K][6]
     float* tproj = nullptr;        // device: [cap][NL][D]
     int tproj_cap = 0;
+    // dpk_sample's per-step temb projections [K][NL][D]: depend only on the weights and the
+    // schedule, so they are computed on the first dpk_sample after either changes and reused
+    float* tps = nullptr;
+    int tps_cap = 0;
+    bool tps_valid = false;
+    hipEvent_t tps_ev = nullptr;   // recorded after the temb launch (other streams wait on it)
+    hipStream_t tps_stream = nullptr;
     std::vector<float> h_arena;    // host staging of the arena
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
@@ -2446,6 +2453,8 @@ void dpk_destroy(dpk_handle* h) {
     if (h->temb) (void)hipFree(h->temb);
     if (h->coef) (void)hipFree(h->coef);
     if (h->tproj) (void)hipFree(h->tproj);
+    if (h->tps) (void)hipFree(h->tps);
+    if (h->tps_ev) (void)hipEventDestroy(h->tps_ev);
     for (auto* v : {&h->ev_used, &h->ev_free})
         for (auto& e : *v) {
             (void)hipEventDestroy(e.first);
@@ -2648,6 +2657,7 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
     }
 #undef GET
     h->have_weights = true;
+    h->tps_valid = false;
     int rc = upload(h);
     if (rc || !pose) return rc;
     // the pose backbone adds no timestep projection: a zero row per layer (E_CHEB1 adds +0)
@@ -2698,6 +2708,7 @@ int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* s
     h->K = K;
     h->eta = eta;
     h->have_sched = true;
+    h->tps_valid = false;
     return DPK_OK;
 }
 
@@ -2752,16 +2763,28 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     if (!h->have_sched) return fail(h, DPK_E_STATE, "schedule not set");
     if (N == 0) return DPK_OK;
     HIPCHK(h, hipSetDevice(h->device));
-    rc = ensure_tproj(h, h->K);
-    if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    if (!h->tps_valid) {
+        if (h->tps_cap < h->K) {
+            if (h->tps) HIPCHK(h, hipFree(h->tps));
+            h->tps = nullptr;
+            HIPCHK(h, hipMalloc(&h->tps, (size_t)h->K * NL * D * 4));
+            h->tps_cap = h->K;
+        }
+        if (!h->tps_ev) HIPCHK(h, hipEventCreateWithFlags(&h->tps_ev, hipEventDisableTiming));
+        hipLaunchKernelGGL(temb_kernel, dim3(h->K), dim3(256), 0, st, h->temb, h->coef + 5, 6, h->tps);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipEventRecord(h->tps_ev, st));
+        h->tps_stream = st;
+        h->tps_valid = true;
+    } else if (st != h->tps_stream && hipEventQuery(h->tps_ev) == hipErrorNotReady) {
+        HIPCHK(h, hipStreamWaitEvent(st, h->tps_ev, 0));
+    }
     if (xs) HIPCHK(h, hipMemcpyAsync(xs, x, (size_t)N * PE * 4, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(temb_kernel, dim3(h->K), dim3(256), 0, st, h->temb, h->coef + 5, 6, h->tproj);
-    HIPCHK(h, hipGetLastError());
     SampleArgs a{};
     a.arena = h->arena;
     a.coef = h->coef;
-    a.tproj = h->tproj;
+    a.tproj = h->tps;
     a.x_in = x;
     a.x_out = out;
     a.xs = xs;

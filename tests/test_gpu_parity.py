@@ -204,3 +204,37 @@ def test_non_h36m_graph_dense_path(mask):
                                 lambda a_, m_, t_: O.gcndiff_forward(O.params_to_torch(sd), O.adjacency(17, edges),
                                                                      a_, m_, t_), _betas(51))
     assert _maxdiff(out, xs[-1]) <= TRAJ_TOL
+
+
+def test_temb_cache_follows_schedule_and_weights(mask):
+    """dpk_sample caches the per-step temb projections; a new schedule or new weights must
+    invalidate them (results equal those of a fresh handle), and repeat calls are exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+    x, _ = synthetic_batch(12, seed=5)
+    xd = torch.from_numpy(x).cuda()
+    sd1, sd2 = synthetic_state_dict(), synthetic_state_dict(seed=7)
+    seq_a, seq_b = make_seq("uniform", 50, 10), make_seq("uniform", 50, 25)
+
+    def fresh(sd, seq):
+        m = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+        m.load_state_dict(sd)
+        out = m.sample(xd, seq, _betas(51), mask=mask).clone()
+        m.close()
+        return out
+
+    m = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+    m.load_state_dict(sd1)
+    a1 = m.sample(xd, seq_a, _betas(51), mask=mask).clone()
+    assert torch.equal(m.sample(xd, seq_a, _betas(51), mask=mask), a1)      # cached projections
+    assert torch.equal(m.sample(xd, seq_b, _betas(51), mask=mask), fresh(sd1, seq_b))
+    m.load_state_dict(sd2)
+    assert torch.equal(m.sample(xd, seq_b, _betas(51), mask=mask), fresh(sd2, seq_b))
+    # another stream after the cache was filled on the current one
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        o = m.sample(xd, seq_b, _betas(51), mask=mask)
+    torch.cuda.synchronize()
+    assert torch.equal(o, fresh(sd2, seq_b))
+    m.close()
