@@ -334,16 +334,15 @@ __device__ __forceinline__ int opaque(int x) {
 
 // ---------------------------------------------------------------------------------------
 // GEMM over the workgroup's 68 rows.  Rows 0..63 are 4 MFMA row tiles (v_mfma_f32_16x16x4_f32);
-// the 4 leftover rows 64..67 ("tail") are computed with scalar v_fma_f32 inside the same k-loop
-// from the B fragments already in registers: one FMA per MFMA, interleaved into the MFMA
-// stream (sched_group_barrier), where a single-issue VALU op hides in the MFMA's issue gap
-// (MI355X_MICROARCH.md: packed f32 ops beside MFMAs cost ~22 cycles each and 4x4x1_16b
-// MFMAs ~20 — both measured slower than this).
+// the 4 leftover rows 64..67 ("tail") run on v_mfma_f32_4x4x1_16b_f32 inside the same k-loop,
+// fed by the B fragments already in registers (TM_MFMA4 below; in a QKV-shaped k-block the 20
+// tail MFMAs cost 8.8 cycles each beside the 72 16x16x4 ones, tools/mfma_mix_probe.hip; VALU
+// FMAs for these rows (v4) cost ~10 cycles each, a padded 16-row tile 25 % of the GEMM).
 //
 // MFMA operand maps: lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for sub-step j,
 // and the packed B block holds W[k = same][n = ct*16 + (l&15)] (a consistent permutation of k).
-// Tail: lane l accumulates, for tail row t and its column (l&15) of col tile c, the partial sum
-// over its own 4 k's of every k-block; the 4 lane groups are summed with two xor-shuffles.
+// Tail: the 4x4x1 accumulators hold partial sums per k-slice (lane group), reduce-scattered by
+// permlane swaps in the epilogue (rs4rows).
 //
 // B blocks are fetched with buffer loads: one VGPR offset (lane*16) shared by every load and the
 // block offset in SGPR soffset, so the k-loop does no VALU address arithmetic.  A comes from one
