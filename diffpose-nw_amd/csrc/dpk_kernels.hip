@@ -95,6 +95,10 @@ constexpr int PE = J * CIN;  // floats per pose (85)
 constexpr int P = DPK_P;     // poses per workgroup
 constexpr int R = P * J;     // 68 (34) rows
 static_assert(P == 4 || P == 2, "4 or 2 poses per workgroup");
+// P = 2 (two workgroups per CU, 34-row GEMMs) was measured slower at v5 (62.4k vs 74k poses/s)
+// and at v9 (72.8k vs 82.6k); the phases added since (MFMA attention, GraphNet MFMA, split-GEMM
+// modes) are written for P = 4, so the option is closed.
+static_assert(P == 4, "DPK_P=2 is no longer maintained (see DESIGN.md section 6)");
 constexpr int WG_PER_CU = P == 4 ? 1 : 2;
 constexpr int NT = 256;      // threads (4 waves, one per SIMD)
 constexpr int NW = NT / 64;
@@ -521,8 +525,9 @@ __device__ __forceinline__ float rcp_nr(float d) {
     return fmaf(r, fmaf(-d, r, 1.0f), r);
 }
 // (mean, 1/(std + eps)) of workgroup row `row` from the partials in st
+template <int RR = R>   // instantiated only by fused-LN kernels (R == 68)
 __device__ __forceinline__ f32x2 ln_row_norm(const float* st, int row) {
-    constexpr int RM = R - R % 16;
+    constexpr int RM = RR - RR % 16;
     float m, M2;
     if (row < RM) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(st + row * 4);
@@ -531,7 +536,7 @@ __device__ __forceinline__ f32x2 ln_row_norm(const float* st, int row) {
         M2 = (v[1] + v[3]) + (d * d) * 24.0f;            // n_a n_b / (n_a + n_b) = 48*48/96
     } else {
         // tail columns per wave (gemm_wave, N = 96): waves 0,1 own 32, waves 2,3 own 16
-        static_assert(R == 68, "tail partial counts");
+        static_assert(RR == 68, "tail partial counts");
         const float* t = st + ST_TAIL + (row - RM) * 16;
         const f32x4 p0 = *reinterpret_cast<const f32x4*>(t), p1 = *reinterpret_cast<const f32x4*>(t + 4);
         const f32x4 p2 = *reinterpret_cast<const f32x4*>(t + 8), p3 = *reinterpret_cast<const f32x4*>(t + 12);
