@@ -1159,9 +1159,10 @@ __device__ __forceinline__ float row_sum(float v) {
 // Rows 0..63: a DPP quad (4 lanes) per row, 16 rows per wave; lane `part` of a row owns the
 // 16-byte chunks part, part+4, ..., part+20 (interleaved across LDS banks).  Rows 64..67: wave w
 // takes row 64+w, 16 lanes x 6 elements (columns 2*lane + 32*e), lanes 16..63 mirror 0..15.
-// Two-pass fp32 statistics; the cross-lane sums are DPP all-reduces whose operands pair up
-// commutatively, so every lane of a row holds bitwise the same mean/std.  Divisions by 96 and
-// 95 and by the row's std use div_by (correctly rounded, as the reference's true division).
+// One-pass fp32 statistics shifted by the row's first element (below); the cross-lane sums are
+// DPP all-reduces whose operands pair up commutatively, so every lane of a row holds bitwise the
+// same mean/std.  The division by the row's std+eps is correctly rounded (div_by with a
+// Newton-refined reciprocal), as the reference's true division.
 __device__ __forceinline__ float quad_sum(float v) {
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
                                                                0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
@@ -1199,52 +1200,56 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
     f32x2 u[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) u[e] = *reinterpret_cast<const f32x2*>(st + 2 * tl + 32 * e);
-    auto psum6 = [](const f32x4 (&x)[6]) {
-        const f32x4 c = ((x[0] + x[1]) + (x[2] + x[3])) + (x[4] + x[5]);
-        return (c[0] + c[1]) + (c[2] + c[3]);
-    };
-    auto psum3 = [](const f32x2 (&x)[3]) {
-        const f32x2 c = (x[0] + x[1]) + x[2];
-        return c[0] + c[1];
-    };
-    const float mean = div_by(quad_sum(psum6(v)), (float)D, RD);
-    const float tmean = div_by(row_sum(psum3(u)), (float)D, RD);
-    f32x4 dv[6], sq[6];
+    // One pass over the row, shifted by its first element c0 (every lane of the row reads the same
+    // value): S1 = sum(x - c0), S2 = sum((x - c0)^2); mean = c0 + S1/96, var = (S2 - S1^2/96)/95
+    // (unbiased, GraFormer.py:64).  With the shift inside the row's range the two sums stay of the
+    // order of the variance, so the one-pass form loses nothing measurable against the two-pass
+    // one, and the two reductions share one DPP chain.
+    const float c0 = s[0], tc0 = st[0];
+    f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
-        dv[e] = v[e] - mean;
-        sq[e] = dv[e] * dv[e];
+        const f32x4 d = v[e] - c0;
+        d1 += d;
+        d2 = __builtin_elementwise_fma(d, d, d2);
     }
-    f32x2 du[3], squ[3];
+    f32x2 e1 = {0.f, 0.f}, e2 = {0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
-        du[e] = u[e] - tmean;
-        squ[e] = du[e] * du[e];
+        const f32x2 d = u[e] - tc0;
+        e1 += d;
+        e2 = __builtin_elementwise_fma(d, d, e2);
     }
-    const float den = sqrtf(div_by(quad_sum(psum6(sq)), (float)(D - 1), RD1)) + LN_EPS;
-    const float tden = sqrtf(div_by(row_sum(psum3(squ)), (float)(D - 1), RD1)) + LN_EPS;
-    const float rcp = 1.0f / den, trcp = 1.0f / tden;
+    const float s1 = quad_sum((d1[0] + d1[1]) + (d1[2] + d1[3]));
+    const float s2 = quad_sum((d2[0] + d2[1]) + (d2[2] + d2[3]));
+    const float t1 = row_sum(e1[0] + e1[1]);
+    const float t2 = row_sum(e2[0] + e2[1]);
+    const float mean = fmaf(s1, RD, c0), tmean = fmaf(t1, RD, tc0);
+    const float var = fmaxf(fmaf(-s1 * RD, s1, s2), 0.f) * RD1;
+    const float tvar = fmaxf(fmaf(-t1 * RD, t1, t2), 0.f) * RD1;
+    const float den = sqrtf(var) + LN_EPS, tden = sqrtf(tvar) + LN_EPS;
+    const float rcp = rcp_nr(den), trcp = rcp_nr(tden);
     float* d = dst + row * LDX;
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
         if (!main_ok) break;
-        const int c0 = 4 * (part + 4 * e);
-        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c0);
-        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c0);
-        const f32x4 t = div_by4(gv * dv[e], den, rcp) + sv;
-        if constexpr (SPLIT) split_store4<SPLIT>(reinterpret_cast<char*>(d), c0, t);
-        else *reinterpret_cast<f32x4*>(d + c0) = t;
+        const int c = 4 * (part + 4 * e);
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c);
+        const f32x4 t = div_by4(gv * (v[e] - mean), den, rcp) + sv;
+        if constexpr (SPLIT) split_store4<SPLIT>(reinterpret_cast<char*>(d), c, t);
+        else *reinterpret_cast<f32x4*>(d + c) = t;
     }
     if (lane < 16 && tail_ok) {
         float* dt = dst + (RM + w) * LDX;
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
-            const int c0 = 2 * tl + 32 * e;
-            const f32x2 gv = *reinterpret_cast<const f32x2*>(gain + c0);
-            const f32x2 sv = *reinterpret_cast<const f32x2*>(shift + c0);
-            const f32x2 t = div_by2(gv * du[e], tden, trcp) + sv;
-            if constexpr (SPLIT) split_store2<SPLIT>(reinterpret_cast<char*>(dt), c0, t);
-            else *reinterpret_cast<f32x2*>(dt + c0) = t;
+            const int c = 2 * tl + 32 * e;
+            const f32x2 gv = *reinterpret_cast<const f32x2*>(gain + c);
+            const f32x2 sv = *reinterpret_cast<const f32x2*>(shift + c);
+            const f32x2 t = div_by2(gv * (u[e] - tmean), tden, trcp) + sv;
+            if constexpr (SPLIT) split_store2<SPLIT>(reinterpret_cast<char*>(dt), c, t);
+            else *reinterpret_cast<f32x2*>(dt + c) = t;
         }
     }
 }
