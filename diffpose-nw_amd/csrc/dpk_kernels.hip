@@ -1661,29 +1661,32 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
     f32x2 v[J];
 #pragma unroll
     for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        f32x2 t1 = {0.f, 0.f}, t2 = {0.f, 0.f};
+    // T1 x = L x; T2 x = (2 L^2 - I) x by the Chebyshev recurrence 2 L (L x) - x (ChebConv.py:90-112
+    // builds T2 as a matrix first; the recurrence needs L's 49 nonzeros twice instead of T2's 87)
+    auto lx = [&](int j, const f32x2 (&u)[J]) {
+        f32x2 acc = {0.f, 0.f};
         if constexpr (SPARSE) {
 #pragma unroll
-            for (int k = 0; k < SPAT.n1[j]; ++k) t1 = pfma(splat2(cw[SPAT.o1[j] + k]), v[SPAT.c1[j][k]], t1);
-#pragma unroll
-            for (int k = 0; k < SPAT.n2[j]; ++k)
-                t2 = pfma(splat2(cw[SPAT.nnz1 + SPAT.o2[j] + k]), v[SPAT.c2[j][k]], t2);
+            for (int k = 0; k < SPAT.n1[j]; ++k) acc = pfma(splat2(cw[SPAT.o1[j] + k]), u[SPAT.c1[j][k]], acc);
         } else {
 #pragma unroll
-            for (int i = 0; i < J; ++i) {
-                t1 = pfma(splat2(cw[j * J + i]), v[i], t1);
-                t2 = pfma(splat2(cw[J * J + j * J + i]), v[i], t2);
-            }
+            for (int i = 0; i < J; ++i) acc = pfma(splat2(cw[j * J + i]), u[i], acc);
         }
+        return acc;
+    };
+    f32x2 t1[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) t1[j] = lx(j, v);
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const f32x2 t2 = pfma(splat2(2.0f), lx(j, t1), -v[j]);
         if constexpr (SPLIT) {
             char* row = reinterpret_cast<char*>(b2 + (p * J + j) * LD2);
-            split_store2<SPLIT>(row, c, t1);
+            split_store2<SPLIT>(row, c, t1[j]);
             split_store2<SPLIT>(row, D + c, t2);
             split_store2<SPLIT>(row, 2 * D + c, v[j]);
         } else {
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1;
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1[j];
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = v[j];
         }
