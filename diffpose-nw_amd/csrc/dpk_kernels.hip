@@ -579,11 +579,16 @@ __device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, fl
 // STATS: the epilogue also writes the fused-LayerNorm partials of its rows (N = 96 only);
 // LNA: the A operand is raw x, normalised in registers with the statistics in `lst` and the
 // gains/shifts lg/lb (LDS) before it feeds the MFMAs (fused LayerNorm, see ln_row_norm).
-template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE, bool STATS = false, bool LNA = false>
+// XS2: k-blocks 0 .. 2S-1 of A come from AX (row stride ldx) instead of A: the Chebyshev GEMMs'
+// T0 = x block is read where x lives (cheb_prep XSKIP).  Those k-blocks are loaded only by the
+// prologue and the peeled first ring pass, so the choice is compile-time.
+template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE, bool STATS = false, bool LNA = false,
+          bool XS2 = false>
 __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* Bp, int rt0, int ct0, int rot,
                                           int trow0, bool tail_dup, int lane, const EpiArgs& e,
                                           const BPre<NCW>& pre, const float* lst = nullptr,
-                                          const float* lg = nullptr, const float* lb = nullptr) {
+                                          const float* lg = nullptr, const float* lb = nullptr,
+                                          const float* AX = nullptr, int ldx = 0) {
     using T = GemmTile<NR, NCW, TM, TR, KB>;
     constexpr int TA = T::TA, NQ = T::NQ;
     static_assert(KB == 1 || KB % 2 == 0, "k-blocks in pairs");
@@ -601,6 +606,13 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     } else {
 #pragma unroll
         for (int i = 0; i < TA; ++i) g.toff[i] = (trow0 + i) * lda + kq;
+    }
+    int xoff[NR], xtoff = 0;
+    if constexpr (XS2) {
+        static_assert(TM == TM_MFMA4, "XS2: 4x4x1 tail rows");
+#pragma unroll
+        for (int i = 0; i < NR; ++i) xoff[i] = ((rt0 + i) * 16 + rl) * ldx + kq;
+        xtoff = (trow0 + (lane & 3)) * ldx + kq;
     }
     int gcol[NCW];                                  // global column tile of local tile c (uniform)
 #pragma unroll
@@ -639,8 +651,19 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     // short (NCW <= 6: 24-48 MFMAs, below the loaded L2 latency), 2 for the 9-tile QKV halves.
     constexpr int S = (KB == 1) ? 1 : (NCW <= 6 && KB % 3 == 0) ? 3 : 2;
     static_assert(KB == 1 || KB % S == 0, "ring slots divide the k-blocks");
+    static_assert(!XS2 || (S == 3 && KB > 2 * S && 2 * S * 16 == D), "XS2: the 96-wide x block is k-blocks 0..5");
     f32x4 as[S][NR], ts[S][TA], bs[S][NCW];
     f32x4 gs[S], ss[S];                         // LNA: gains / shifts of the slot's k's
+    // A k-block kb of slot st: from AX for kb < 2S (XS2), else from A
+    auto loadA = [&](int st, int kb) {
+        if (XS2 && kb < 2 * S) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) as[st][i] = *reinterpret_cast<const f32x4*>(AX + xoff[i] + kb * 16);
+            ts[st][0] = *reinterpret_cast<const f32x4*>(AX + xtoff + kb * 16);
+        } else {
+            g.loadA(as[st], ts[st], A, kb);
+        }
+    };
     f32x2 nrm[NR], tnrm = {0.f, 0.f};           // LNA: (mean, 1/(std+eps)) of the lane's rows
     if constexpr (LNA) {
         static_assert(TM == TM_MFMA4, "fused LN operand: 4x4x1 tail rows");
@@ -684,7 +707,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
     for (int st = 2; st < S; ++st) T::loadB(bs[st], src, soff, st);
 #pragma unroll
     for (int st = 0; st < S; ++st) {
-        g.loadA(as[st], ts[st], A, st);
+        loadA(st, st);
         loadLN(st, st);
     }
     lnx(0);
@@ -695,7 +718,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
             if (st == 0) mma_first();
             else mma(st);
             T::loadB(bs[st], src, soff, st + S);
-            g.loadA(as[st], ts[st], A, st + S);
+            loadA(st, st + S);
             loadLN(st, st + S);
             T::schedule_half();
         }
@@ -817,18 +840,19 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
 // Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
 // 2*(w>>1)+1 and column half w&1 on the 16x16x4 MFMA; the 4 tail rows 64..67 of that column
 // half on 4x4x1 MFMAs, split between the half's two waves (rotated column order for w>>1 = 1).
-template <int NC, int KB, int MODE, bool STATS = false, bool LNA = false>
+template <int NC, int KB, int MODE, bool STATS = false, bool LNA = false, bool XS2 = false>
 __device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp, int wave, int lane,
                                         const EpiArgs& e, const BPre<NC / 2>& pre, const float* lst = nullptr,
-                                        const float* lg = nullptr, const float* lb = nullptr) {
+                                        const float* lg = nullptr, const float* lb = nullptr,
+                                        const float* AX = nullptr, int ldx = 0) {
     static_assert(NC % 2 == 0 && (R == 68 || R == 34) && NW == 4, "row tiles x 2 column halves + tail rows");
     constexpr int NCW = NC / 2;
     constexpr int NRW = R == 68 ? 2 : 1;            // row tiles per wave
     const int pr = gemm_pr(wave);
     const bool dup = (NCW & 1) && pr == 1;
-    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE, STATS, LNA>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW,
-                                                               col_rot<NCW>(wave), R - R % 16, dup, lane, e, pre,
-                                                               lst, lg, lb);
+    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE, STATS, LNA, XS2>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW,
+                                                                    col_rot<NCW>(wave), R - R % 16, dup, lane, e,
+                                                                    pre, lst, lg, lb, AX, ldx);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1649,7 +1673,9 @@ static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
 // earlier LDS writes produced when it follows graph_mma (no workgroup barrier in between).
 // SPARSE: compile-time pattern, packed values (scalar loads); dense: 17x17 from the arena.
 // Sums run over increasing i in both (identical bits).
-template <bool SPARSE, int SPLIT = 0>
+// XSKIP (fp32 GEMM mode, Cheb1/Cheb2): write [- | T1 src | T2 src] and let the GEMM read the
+// T0 = src part from src itself (gemm_wave XS2), saving a third of the stores.
+template <bool SPARSE, int SPLIT = 0, bool XSKIP = false>
 __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int wave,
                                           int lane) {
     lane = opaque(lane);
@@ -1685,6 +1711,9 @@ __device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const fl
             split_store2<SPLIT>(row, c, t1[j]);
             split_store2<SPLIT>(row, D + c, t2);
             split_store2<SPLIT>(row, 2 * D + c, v[j]);
+        } else if constexpr (XSKIP) {
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t1[j];
+            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = t2;
         } else {
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1[j];
             *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
@@ -2066,9 +2095,11 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
                     BAR();
                     if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
-                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, XS, B2, wave, lane);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, 0, true>(CW, XS, B2, wave, lane);
                     BAR();
-                    if (DPK_RUN(16 | 512)) gemm_wg<6, 18, E_CHEB1>(B2, LD2, LW + OFF_C1, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 512))
+                        gemm_wg<6, 18, E_CHEB1, false, false, true>(B2, LD2, LW + OFF_C1, wave, lane, e, pre, nullptr,
+                                                                    nullptr, nullptr, XS, LDX);
                 }
             }
             {
@@ -2083,11 +2114,13 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 } else {
                     const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
                     BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE>(CW, B1, B2, wave, lane);
+                    if (DPK_RUN(4)) cheb_prep<SPARSE, 0, true>(CW, B1, B2, wave, lane);
                     BAR();
                     if constexpr (LNF)
                         if (l + 1 < NL) qpre = gemm_prefetch<18, 6>(LW + LAYER_FLOATS + OFF_QKV, wave, lane);
-                    if (DPK_RUN(16 | 1024)) gemm_wg<6, 18, E_RESID_RELU, LNF>(B2, LD2, LW + OFF_C2, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 1024))
+                        gemm_wg<6, 18, E_RESID_RELU, LNF, false, true>(B2, LD2, LW + OFF_C2, wave, lane, e, pre,
+                                                                       ST, nullptr, nullptr, B1, LDX);
                 }
             }
             BAR();
@@ -2587,9 +2620,11 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         pack_blocks(Lw + OFF_O, D, D, KB_D, 6, [&](int k, int n) { return wo[n * D + k]; });
         pack_blocks(Lw + OFF_FC1, D, D2, KB_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
         pack_blocks(Lw + OFF_FC2, D2, D, KB_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
-        // ChebConv weight (3,1,in,out), rows in cheb_prep's B2 order [T1X | T2X | X]: k -> order (k/96+1)%3
-        pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; });
-        pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; });
+        // ChebConv weight (3,1,in,out): the fp32 GEMMs read [x | T1x | T2x] (x from its own buffer,
+        // cheb_prep XSKIP), the reference's row order; the split GEMMs read cheb_prep's one-buffer
+        // [T1x | T2x | x] (cheb_row)
+        pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[k * D + n]; });
+        pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[k * D + n]; });
         uint16_t* L16 = h->h_arena16.data() + (size_t)l * LAYER16_BYTES / 2;
         w16max = fmaxf(w16max, pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
             const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
