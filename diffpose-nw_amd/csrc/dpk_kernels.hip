@@ -1817,18 +1817,18 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
             for (int t = 0; t < 6; ++t) a[t][s] = fmaf((a[t][s] - nrm[0]) * nrm[1], gn[t], sh[t]);
         }
     }
+    // k-steps outer, tiles inner: consecutive MFMAs are independent (no 5-deep dependent chain
+    // per tile); the first k-step starts from C = 0
     f32x4 acc[6];
     float p16[6];
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
-        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        p16[t] = 0.f;
+    for (int s = 0; s < 5; ++s)
 #pragma unroll
-        for (int s = 0; s < 5; ++s) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], lb[s], acc[t], 0, 0, 0);
-            p16[t] = fmaf(l16[s], a[t][s], p16[t]);
+        for (int t = 0; t < 6; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], lb[s], s == 0 ? z : acc[t], 0, 0, 0);
+            p16[t] = s == 0 ? l16[0] * a[t][0] : fmaf(l16[s], a[t][s], p16[t]);
         }
-    }
     const int row_j = wave * J + cl, row16 = wave * J + 16;
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
