@@ -199,3 +199,25 @@ def test_gcnpose_oracle(golden, graph):
     assert np.array_equal(xyz.numpy(), g["xyz"])
     assert np.array_equal(O.gcnpose_forward(P, graph, x2d, torch.from_numpy(g["mask2"])).numpy(), g["xyz_masked"])
     assert np.array_equal(O.build_uvxyz(x2d, xyz, 3, "quirk").numpy(), g["uvxyz_h3"])
+
+
+def test_load_checkpoint_reference_format(tmp_path):
+    """A checkpoint shaped like the reference's (runners/diffpose_frame.py:131-132: torch.save of a list
+    whose [0] is the DataParallel state_dict, "module." prefixed) loads with weights_only=True."""
+    import torch
+
+    from diffpose_amd.weights import load_checkpoint
+
+    sd = synthetic_state_dict()
+    states = [{"module." + k: torch.from_numpy(v.copy()) for k, v in sd.items()},
+              {"state": {}, "param_groups": [{"lr": 1e-3, "params": [0, 1]}]}]
+    path = tmp_path / "ckpt_diff.pth"
+    torch.save(states, str(path))
+    got = load_checkpoint(str(path), kind="diff")
+    assert list(got.keys()) == list(sd.keys())
+    assert all(np.array_equal(got[k], sd[k]) for k in sd)
+    # GCNpose checkpoints use the same container (diffpose_frame.py:146-147)
+    psd = synthetic_state_dict(kind="pose")
+    torch.save([{"module." + k: torch.from_numpy(v.copy()) for k, v in psd.items()}], str(path))
+    gp = load_checkpoint(str(path), kind="pose")
+    assert all(np.array_equal(gp[k], psd[k]) for k in psd)
