@@ -113,7 +113,8 @@ constexpr int SM_XST = SM_B2 + R * LD2;     // pose state x_t    [R][5]
 constexpr int SM_LNP = SM_XST + ((R * CIN + 3) / 4) * 4;   // LayerNorm gains/shifts of all layers [NL][4][D]
 constexpr int SM_ST = SM_LNP + NL * 4 * D;                  // LayerNorm row statistics (fused LN, below)
 constexpr int ST_TAIL = 64 * 4;                             // [64 main rows][mean0, M2_0, mean1, M2_1]
-constexpr int SM_FLOATS = SM_ST + ST_TAIL + 4 * 4 * 4;      // + [4 tail rows][4 waves][n, mean, M2, -]
+constexpr int SM_TC = SM_ST + ST_TAIL + 4 * 4 * 4;          // + [4 tail rows][4 waves][n, mean, M2, -]
+constexpr int SM_FLOATS = SM_TC + 2 * J * J;                // dense T1, T2 for the output ChebConv
 static_assert(SM_FLOATS * 4 <= 160 * 1024, "LDS budget");
 
 // packed-weight blocks: one block = 16 cols x 16 k = 64 lanes x float4
@@ -1120,7 +1121,7 @@ __device__ __forceinline__ BPre<1> out_prefetch(const float* Bp, int lane) {
     return pre;
 }
 
-template <int KB, class Epi>
+template <int KB, int NCOL, class Epi>
 __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* Bp, int wave, int lane, Epi epi,
                                          const BPre<1>& pre) {
     using T = GemmTile<1, 1, TM_VALU, 1, KB, false>;
@@ -1149,7 +1150,7 @@ __device__ __forceinline__ void gemm_out(const float* A, int lda, const float* B
     g.mma(a0, t0, b0);
     g.mma(a1, t1, b1);
     const float tv = sum4rows(g.tl[0][0]);
-    if (rl < COUT) {
+    if (rl < NCOL) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) epi(wave * 16 + kq + r, rl, g.acc[0][0][r]);
         if (kq == 0) epi(R - R % 16 + wave, rl, tv);
@@ -1936,6 +1937,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
     // are not wave-uniform, and as global loads their L2 latency sat on the LN critical path)
     static_assert(OFF_LN0B == OFF_LN0A + D && OFF_LN1A == OFF_LN0A + 2 * D && OFF_LN1B == OFF_LN0A + 3 * D, "LN block");
     for (int i = tid; i < NL * 4 * D; i += NT) LNP[i] = W[(i / (4 * D)) * LAYER_FLOATS + OFF_LN0A + i % (4 * D)];
+    for (int i = tid; i < 2 * J * J; i += NT) sm[SM_TC + i] = W[OFF_CHEB + i];
     if (WG_PER_CU == 2 && a.phase_delay > 0 && blockIdx.x >= (gridDim.x + 1) / 2) {
         // de-phase the two co-resident workgroups of a CU so one runs its VALU phases while the
         // other runs MFMA phases (the dispatcher fills second CU slots with the grid's second half)
@@ -2126,9 +2128,14 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             BAR();
         }
         // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
-        //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly)
-        const auto preo = out_prefetch<18>(W + OFF_WOUT, lane);
-        cheb_prep<SPARSE>(CW, XS, B2, wave, lane);
+        //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly).
+        //      sum_k T_k x W_k computed as sum_k T_k (x W_k): one K=96 GEMM Y = x [W0 | W1 | W2]
+        //      (3*cout columns, one tile) into B2, then the 17x17 products on the 3*cout columns.
+        constexpr int COUTK = POSE ? COUT_POSE : COUT;
+        const auto preo = out_prefetch<KB_D>(W + OFF_WOUT, lane);
+        if (wave < R / 16)
+            gemm_out<KB_D, 3 * COUTK>(XS, LDX, W + OFF_WOUT, wave, lane,
+                                      [&](int r, int c, float v) { B2[r * LD2 + c] = v; }, preo);
         BAR();
         {
             float cf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2137,12 +2144,23 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
 #pragma unroll
                 for (int i = 0; i < 5; ++i) cf[i] = cfp[i];                  // uniform: SGPRs
             }
-            const float bo = W[OFF_BOUT + (lane & 15)];
-            auto epi = [&](int r, int c, float v) {
-                const float et = v + bo;
-                const int idx = r * CIN + c;           // same as r*COUT+c (coords 5 -> 5)
-                const bool valid = idx < nvalid;
-                const size_t gidx = (size_t)pose0 * PE + idx;
+            const float* T1d = sm + SM_TC;
+            const float* T2d = T1d + J * J;
+            for (int idx = tid; idx < P * J * COUTK; idx += NT) {
+                const int p = idx / (J * COUTK), rem = idx - p * (J * COUTK);
+                const int j = rem / COUTK, c = rem - j * COUTK;
+                const float* yp = B2 + p * J * LD2;
+                float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+                for (int i = 0; i < J; ++i) {
+                    a1 = fmaf(T1d[j * J + i], yp[i * LD2 + COUTK + c], a1);
+                    a2 = fmaf(T2d[j * J + i], yp[i * LD2 + 2 * COUTK + c], a2);
+                }
+                const float et = ((yp[j * LD2 + c] + a1) + a2) + W[OFF_BOUT + c];
+                const int r = p * J + j;
+                const int oidx = r * CIN + c;          // same as r*COUT+c (coords 5 -> 5)
+                const bool valid = oidx < nvalid;
+                const size_t gidx = (size_t)pose0 * PE + oidx;
                 if (POSE) {
                     B1[r * LDX + c] = et;
                 } else if (EPS_MODE) {
@@ -2150,15 +2168,14 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                 } else {
                     const float z = a.eta != 0.f ? normal_noise(a.seed, s, (long long)gidx) : 0.f;
                     float x0, xn;
-                    ddim_elem(cf, XST[idx], et, z, x0, xn);
-                    XST[idx] = xn;
+                    ddim_elem(cf, XST[oidx], et, z, x0, xn);
+                    XST[oidx] = xn;
                     if (valid) {
                         if (a.x0s) a.x0s[(size_t)s * a.N * PE + gidx] = x0;
                         if (a.xs) a.xs[(size_t)(s + 1) * a.N * PE + gidx] = xn;
                     }
                 }
-            };
-            if (wave < R / 16) gemm_out<18>(B2, LD2, W + OFF_WOUT, wave, lane, epi, preo);
+            }
         }
         BAR();
     }
@@ -2686,7 +2703,9 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         const int o = k / CIN, c = k % CIN;
         return c < cin ? wi[o * cin * D + c * D + n] : 0.f;
     });
-    pack_blocks(A + OFF_WOUT, D3, cout, KB_D3, 1, [&](int k, int n) { return wout[cheb_row(k) * cout + n]; });
+    // output ChebConv as Y = x [W0 | W1 | W2] (96 -> 3*cout columns), out = Y0 + T1 Y1 + T2 Y2 in the kernel
+    pack_blocks(A + OFF_WOUT, D, 3 * cout, KB_D, 1,
+                [&](int k, int n) { return wout[((n / cout) * D + k) * cout + n % cout]; });
     for (int c = 0; c < D; ++c) A[OFF_BIN + c] = bi[c];
     for (int c = 0; c < 16; ++c) A[OFF_BOUT + c] = c < cout ? bout[c] : 0.f;
     if (!pose) {         // GCNpose carries temb.dense too (gcnpose.py:94-98) but never uses it

@@ -46,7 +46,7 @@ def _events(gemm_mode="fp32", fused=None):
         gemm(p + "fc2"); bar(p + "fc2")
         bar(p + "graph2+cheb1"); gemm(p + "C1"); bar(p + "C1")
         bar(p + "cheb_prep2"); gemm(p + "C2"); bar(p + "C2")
-    bar("cheb_out"); bar("out_gemm+ddim")
+    bar("out_gemm"); bar("out_graph+ddim")
     return ev
 
 
