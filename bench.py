@@ -101,7 +101,10 @@ def main():
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under a launcher (torch.distributed.run sets RANK/MASTER_ADDR) the RCCL path runs at every
+    # N, N=1 included, so per-GPU work is the same at every point of the scaling sweep
+    use_dist = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     # ---- model, schedule, inputs (synthetic, seeded) ----
@@ -122,7 +125,7 @@ def main():
 
     def step():
         model.sample(x, seq, betas, eta=args.eta, out=out)
-        if world > 1:                            # the one data-path collective: final poses to every rank
+        if use_dist:                             # the one data-path collective: final poses to every rank
             D.gather_frames(out, B_total, args.hyp)
 
     def measure(gemm):
@@ -146,14 +149,14 @@ def main():
         else:
             run = step
             model.profile(True)
-        if world > 1:
+        if use_dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             run()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_dist:
             dist.barrier()
         elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
         kernel_ms = model.kernel_times_ms() if graph is None else []
@@ -216,7 +219,7 @@ def main():
         "config": {"workload": f"human36m_diffpose_uvxyz_cpn eval: {args.frames} frames/GPU x H={args.hyp}, "
                                f"K={K} DDIM (uniform skip over T'={args.T_test}, T={args.T}), eta={args.eta}",
                    "frames_per_gpu": args.frames, "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
-                   "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if world > 1 else ""),
+                   "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if use_dist else ""),
                    "hipgraph": bool(args.graph), "gemm": args.gemm},
         "roofline": roof,
         "cpu_baseline": None,
@@ -276,7 +279,7 @@ def main():
         v.pop("_out", None)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
