@@ -1210,27 +1210,37 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
     tid = opaque(tid);
     const int w = tid >> 6, lane = tid & 63;
     constexpr float RD = 1.0f / (float)D, RD1 = 1.0f / (float)(D - 1);
-    // ---- rows 0..63 (0..31 at P=2: waves 2-3 compute row 31 and store nothing)
+    // ---- rows 0..63: wave w rows 16w..16w+15; row 64 + w: the tail row of wave w
     constexpr int RM = R - R % 16, RT = R % 16;
-    static_assert(RT <= 4, "tail rows: one per wave");
-    const bool main_ok = w * 16 < RM, tail_ok = w < RT;
-    const int row = main_ok ? w * 16 + (lane >> 2) : RM - 1, part = lane & 3;
+    static_assert(RM == 64 && RT == NW, "4 row tiles + one tail row per wave");
+    const int row = w * 16 + (lane >> 2), part = lane & 3;
     const float* s = src + row * LDX;
-    f32x4 v[6];
+    const int tl = lane & 15;
+    const float* st = src + (RM + w) * LDX;
+    // the row chunks, and the gains/shifts of the lane's columns, all issued up front: the
+    // normalisation then waits on no LDS round trip (one per chunk when they were read there)
+    f32x4 v[6], gv[6], sv[6];
+    f32x2 u[3], tg[3], tsh[3];
 #pragma unroll
     for (int e = 0; e < 6; ++e) v[e] = *reinterpret_cast<const f32x4*>(s + 4 * (part + 4 * e));
-    // ---- row 64 + w
-    const int tl = lane & 15;
-    const float* st = src + (RM + (tail_ok ? w : 0)) * LDX;
-    f32x2 u[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) u[e] = *reinterpret_cast<const f32x2*>(st + 2 * tl + 32 * e);
+    const float c0 = s[0], tc0 = st[0];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        gv[e] = *reinterpret_cast<const f32x4*>(gain + 4 * (part + 4 * e));
+        sv[e] = *reinterpret_cast<const f32x4*>(shift + 4 * (part + 4 * e));
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        tg[e] = *reinterpret_cast<const f32x2*>(gain + 2 * tl + 32 * e);
+        tsh[e] = *reinterpret_cast<const f32x2*>(shift + 2 * tl + 32 * e);
+    }
     // One pass over the row, shifted by its first element c0 (every lane of the row reads the same
     // value): S1 = sum(x - c0), S2 = sum((x - c0)^2); mean = c0 + S1/96, var = (S2 - S1^2/96)/95
     // (unbiased, GraFormer.py:64).  With the shift inside the row's range the two sums stay of the
     // order of the variance, so the one-pass form loses nothing measurable against the two-pass
     // one, and the two reductions share one DPP chain.
-    const float c0 = s[0], tc0 = st[0];
     f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
@@ -1257,22 +1267,18 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
     float* d = dst + row * LDX;
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
-        if (!main_ok) break;
         const int c = 4 * (part + 4 * e);
-        const f32x4 gv = *reinterpret_cast<const f32x4*>(gain + c);
-        const f32x4 sv = *reinterpret_cast<const f32x4*>(shift + c);
-        const f32x4 t = div_by4(gv * (v[e] - mean), den, rcp) + sv;
+        const f32x4 t = div_by4(gv[e] * (v[e] - mean), den, rcp) + sv[e];
         if constexpr (SPLIT) split_store4<SPLIT>(reinterpret_cast<char*>(d), c, t);
         else *reinterpret_cast<f32x4*>(d + c) = t;
     }
-    if (lane < 16 && tail_ok) {
-        float* dt = dst + (RM + w) * LDX;
+    // the tail row: lanes 16..63 mirror 0..15 and store nothing
+    float* dt = dst + (RM + w) * LDX;
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-            const int c = 2 * tl + 32 * e;
-            const f32x2 gv = *reinterpret_cast<const f32x2*>(gain + c);
-            const f32x2 sv = *reinterpret_cast<const f32x2*>(shift + c);
-            const f32x2 t = div_by2(gv * (u[e] - tmean), tden, trcp) + sv;
+    for (int e = 0; e < 3; ++e) {
+        const int c = 2 * tl + 32 * e;
+        const f32x2 t = div_by2(tg[e] * (u[e] - tmean), tden, trcp) + tsh[e];
+        if (lane < 16) {
             if constexpr (SPLIT) split_store2<SPLIT>(reinterpret_cast<char*>(dt), c, t);
             else *reinterpret_cast<f32x2*>(dt + c) = t;
         }
@@ -1771,15 +1777,28 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
 //   SPLIT_OUT: out written split-fp16 into rows of stride LD2 (gemm mode 1, graph1)
 //   else:      dst (stride LDX) = out (in place allowed: each wave reads its rows before writing)
 // The fragments are loaded one phase ahead (gfrag_load) so their L2 latency hides there.
+// BIAS (graph2): also the lane's fc2 bias columns, so the RESID epilogue waits on no global load.
 struct GFrag {
     float lb[5], l16[5];
+    f32x4 b4[6];
+    float b1[6];
 };
-__device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int lane) {
+template <bool BIAS = false>
+__device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int lane,
+                                            const float* __restrict__ bias = nullptr) {
     GFrag f;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
         f.lb[s] = LF[s * 64 + lane];
         f.l16[s] = LF[(5 + s) * 64 + lane];
+    }
+    if constexpr (BIAS) {
+        const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
+            f.b1[t] = bias[16 * t + cl];
+        }
     }
     return f;
 }
@@ -1797,6 +1816,17 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
     const float(&lb)[5] = f.lb;
     const float(&l16)[5] = f.l16;
     const float* xp = src + wave * J * LDX + cl;
+    const int row_j = wave * J + cl, row16 = wave * J + 16;
+    // RESID: the residual rows this lane updates, read before the MFMAs (dst != src)
+    f32x4 old[6];
+    float old16[6];
+    if constexpr (RESID) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            old[t] = *reinterpret_cast<const f32x4*>(dst + row_j * LDX + 16 * t + 4 * g);
+            old16[t] = dst[row16 * LDX + 16 * t + cl];
+        }
+    }
     float a[6][5];
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
@@ -1830,15 +1860,13 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], lb[s], s == 0 ? z : acc[t], 0, 0, 0);
             p16[t] = s == 0 ? l16[0] * a[t][0] : fmaf(l16[s], a[t][s], p16[t]);
         }
-    const int row_j = wave * J + cl, row16 = wave * J + 16;
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
         const int c0 = 16 * t + 4 * g;
         if constexpr (SPLIT_OUT) {
             split_store4<SPLIT_OUT>(reinterpret_cast<char*>(dst + row_j * LD2), c0, acc[t]);
         } else if constexpr (RESID) {
-            f32x4* o = reinterpret_cast<f32x4*>(dst + row_j * LDX + c0);
-            *o = *o + (acc[t] + *reinterpret_cast<const f32x4*>(bias + c0));
+            *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = old[t] + (acc[t] + f.b4[t]);
         } else {
             *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = acc[t];
         }
@@ -1853,7 +1881,7 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
             if constexpr (SPLIT_OUT) {
                 split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c, v16[t]);
             } else if constexpr (RESID) {
-                dst[row16 * LDX + c] = dst[row16 * LDX + c] + (v16[t] + bias[c]);
+                dst[row16 * LDX + c] = old16[t] + (v16[t] + f.b1[t]);
             } else {
                 dst[row16 * LDX + c] = v16[t];
             }
@@ -2067,7 +2095,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     gemm_wg<12, 6, E_STORE_RELU>(B1, LDX, LW + OFF_FC1, wave, lane, e, pre);
                 }
             }
-            const GFrag gf2 = gfrag_load(LW + OFF_LGF, lane);   // graph2's operands, a GEMM ahead
+            const GFrag gf2 = gfrag_load<true>(LW + OFF_LGF, lane, LW + OFF_BFC2);   // graph2's operands, a GEMM ahead
             {
                 const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
