@@ -698,6 +698,26 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         g.template mma<true>(as[0], ts[0], bs[0]);
         if constexpr (LNA) lnx(S > 1 ? 1 : 0);
     };
+    // residual epilogues: the wave's own output tiles of dst (its rows 64..67 columns too), read
+    // before the last ring pass so the epilogue waits on no LDS round trip (the GEMM's A operand
+    // is never dst, and no other wave writes these tiles before this wave's epilogue)
+    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
+    const int trow = trow0 + (lane & 3);
+    f32x4 old[NR][NCW];
+    float oldt[NQ];
+    auto load_old = [&]() {
+        if constexpr (RES) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i)
+#pragma unroll
+                for (int c = 0; c < NCW; ++c)
+                    old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
+            if constexpr (TM == TM_MFMA4) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) oldt[q] = e.dst[min(trow, R - 1) * e.ldd + gcol[q] * 16 + tcol];
+            }
+        }
+    };
 #pragma unroll
     for (int c = 0; c < NCW; ++c) {
         bs[0][c] = pre.b0[c];
@@ -734,12 +754,14 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
                 T::schedule_half();
             }
         }
+        load_old();
 #pragma unroll
         for (int st = 0; st < S; ++st) {
             g.mma(as[st], ts[st], bs[st]);
             if (st + 1 < S) lnx(st + 1);
         }
     } else {
+        load_old();
 #pragma unroll
         for (int st = 0; st < S; ++st) {
             if (st == 0) g.template mma<true>(as[st], ts[st], bs[st]);
@@ -748,21 +770,12 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         }
     }
     DPK_GEMM_HOOK(1);
-    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
     auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
         if constexpr (MODE != E_CHEB1) return f32x4{0.f, 0.f, 0.f, 0.f};
         if (e.tproj_pose_stride == 0) return uniform4;
         const int pose = min(e.pose0 + row / J, e.pose_max);
         return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
     };
-    f32x4 old[NR][NCW];
-    if constexpr (RES) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < NCW; ++c)
-                old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
-    }
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
         const int row = (rt0 + i) * 16 + rl;
@@ -797,7 +810,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         static_assert(TM != TM_VALU, "gemm_wave computes transposed tiles; VALU tails are gemm_out's");
     } else if constexpr (TM == TM_MFMA4) {
         // reduce-scatter the 4 k-slices: lane l then holds tail row l&3, column tcol of tile q
-        const int row = trow0 + (lane & 3);
+        const int row = trow;
         float tv[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -806,9 +819,8 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
             if ((q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
             const int col = gcol[q] * 16 + tcol;
             float* dp = e.dst + row * e.ldd + col;
-            const float oldt = RES ? *dp : 0.f;
             const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
-            tv[q] = epi_value<MODE>(v, tbias[q], tp, oldt);
+            tv[q] = epi_value<MODE>(v, tbias[q], tp, RES ? oldt[q] : 0.f);
             *dp = tv[q];
         }
         if constexpr (STATS) {
@@ -1444,25 +1456,26 @@ __device__ __forceinline__ float max4rows(float v) {
 //            the permuted order the scores left them in), so lane (g, c) ends with
 //            O[query c][dims 4g..4g+3] of the tile: one 16-byte store; key 16 added by FMA;
 //   query 16 lane (g, c) forms p16[c] * V[c][6g..6g+5], summed over the DPP row.
-// Same arithmetic as the reference (scores / sqrt(d_k) by correctly rounded division,
-// masked keys -1e9, softmax, P.V), fp32 throughout; only the summation orders differ.
+// The reference's arithmetic (scores / sqrt(d_k), masked keys -1e9, softmax, P.V) in fp32, with
+// the scale taken as one multiply by log2(e)/sqrt(d_k) and exp(x) as 2^x (v_exp_f32): the
+// softmax is invariant to the base, so only roundings and summation orders differ.
 template <int SPLIT = 0>
 __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsigned mask, int wave, int lane) {
     lane = opaque(lane);
     if (wave >= P) return;
     const int g = lane >> 4, c = lane & 15;
-    const float rcp_sdk = 1.0f / SQRT_DK;
     constexpr float LOG2E = 1.4426950408889634f;
+    const float sl = (1.0f / SQRT_DK) * LOG2E;      // scores in log2 units: exp(s/sqrt(dk)) = 2^(dot*sl)
     const float* prow = qkv + wave * J * LD2;
     float* orow = out + wave * J * LDX;
     const bool kok16 = ((mask >> 16) & 1u) != 0u;
     bool kokr[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) kokr[r] = ((mask >> (4 * g + r)) & 1u) != 0u;
-    // scores / sqrt(d_k), masked keys -1e9 (GraFormer.py:104-106); exp as 2^(x log2 e) on
-    // v_exp_f32 (the softmax's max is subtracted first, so x <= 0)
-    auto scale = [&](float dot, bool ok) { return ok ? dot * rcp_sdk : -1e9f; };
-    auto ex = [&](float x) { return __builtin_amdgcn_exp2f(x * LOG2E); };
+    // scores / sqrt(d_k), masked keys -1e9 (GraFormer.py:104-106), kept in log2 units (scaled by
+    // log2 e with the 1/sqrt(d_k)) so the softmax's exp is one v_exp_f32 (2^x) of (score - max) <= 0
+    auto scale = [&](float dot, bool ok) { return ok ? dot * sl : -1e9f; };
+    auto ex = [&](float x) { return __builtin_amdgcn_exp2f(x); };
     // The 4 heads are independent: every stage below runs over all of them before the next
     // stage, so the in-order issue interleaves 4 dependency chains (MFMA accumulations,
     // permlane reductions, exp) instead of waiting out one head's latencies at a time.
@@ -2160,7 +2173,11 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
         //      sum_k T_k x W_k computed as sum_k T_k (x W_k): one K=96 GEMM Y = x [W0 | W1 | W2]
         //      (3*cout columns, one tile) into B2, then the 17x17 products on the 3*cout columns.
         constexpr int COUTK = POSE ? COUT_POSE : COUT;
+        constexpr int NOUT = P * J * COUTK, NIT = (NOUT + NT - 1) / NT;
         const auto preo = out_prefetch<KB_D>(W + OFF_WOUT, lane);
+        float bo[NIT];                                  // output bias of this thread's outputs, a GEMM ahead
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) bo[k] = W[OFF_BOUT + (tid + k * NT) % COUTK];
         if (wave < R / 16)
             gemm_out<KB_D, 3 * COUTK>(XS, LDX, W + OFF_WOUT, wave, lane,
                                       [&](int r, int c, float v) { B2[r * LD2 + c] = v; }, preo);
@@ -2174,7 +2191,10 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             }
             const float* T1d = sm + SM_TC;
             const float* T2d = T1d + J * J;
-            for (int idx = tid; idx < P * J * COUTK; idx += NT) {
+#pragma unroll
+            for (int k = 0; k < NIT; ++k) {
+                const int idx = tid + k * NT;
+                if (idx >= NOUT) break;
                 const int p = idx / (J * COUTK), rem = idx - p * (J * COUTK);
                 const int j = rem / COUTK, c = rem - j * COUTK;
                 const float* yp = B2 + p * J * LD2;
@@ -2184,7 +2204,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     a1 = fmaf(T1d[j * J + i], yp[i * LD2 + COUTK + c], a1);
                     a2 = fmaf(T2d[j * J + i], yp[i * LD2 + 2 * COUTK + c], a2);
                 }
-                const float et = ((yp[j * LD2 + c] + a1) + a2) + W[OFF_BOUT + c];
+                const float et = ((yp[j * LD2 + c] + a1) + a2) + bo[k];
                 const int r = p * J + j;
                 const int oidx = r * CIN + c;          // same as r*COUT+c (coords 5 -> 5)
                 const bool valid = oidx < nvalid;
