@@ -89,6 +89,9 @@ constexpr int PE = J * CIN;  // floats per pose (85)
 #ifndef DPK_LN_FUSE
 #define DPK_LN_FUSE 0        // 1: fp32 mode: LayerNorm statistics from the producing GEMM epilogue, applied in the consumer
 #endif
+#ifndef DPK_LN1_FUSE
+#define DPK_LN1_FUSE 0       // 1: as DPK_LN_FUSE for LN1 only (O-proj epilogue statistics, applied by graph1)
+#endif
 #ifndef DPK_P
 #define DPK_P 4              // poses per workgroup: 4 (one workgroup per CU) or 2 (two per CU)
 #endif
@@ -1274,7 +1277,7 @@ __device__ __forceinline__ void layer_norm(const float* src, float* dst, const f
     const float mean = fmaf(s1, RD, c0), tmean = fmaf(t1, RD, tc0);
     const float var = fmaxf(fmaf(-s1 * RD, s1, s2), 0.f) * RD1;
     const float tvar = fmaxf(fmaf(-t1 * RD, t1, t2), 0.f) * RD1;
-    const float den = sqrtf(var) + LN_EPS, tden = sqrtf(tvar) + LN_EPS;
+    const float den = __builtin_amdgcn_sqrtf(var) + LN_EPS, tden = __builtin_amdgcn_sqrtf(tvar) + LN_EPS;   // v_sqrt_f32 (1 ulp)
     const float rcp = rcp_nr(den), trcp = rcp_nr(tden);
     float* d = dst + row * LDX;
 #pragma unroll
@@ -1815,6 +1818,15 @@ __device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int la
     }
     return f;
 }
+// the bias part alone (issued a phase earlier than the fragments, see the kernel)
+__device__ __forceinline__ void gbias_load(GFrag& f, const float* __restrict__ bias, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
+        f.b1[t] = bias[16 * t + cl];
+    }
+}
 
 // LNA: src is raw x; the operand is LayerNorm(x) formed in registers (fused LN1: statistics
 // from the O-proj epilogue in lst, gains/shifts ng/nb in LDS; see ln_row_norm).
@@ -1956,6 +1968,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
     float* LNP = sm + SM_LNP;
     float* ST = sm + SM_ST;
     constexpr bool LNF = DPK_LN_FUSE && G16 == 0 && R == 68;   // fused LayerNorm (fp32 GEMM mode)
+    constexpr bool LN1F = LNF || (DPK_LN1_FUSE && G16 == 0 && R == 68);   // LN1 alone fused into graph1
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
@@ -2070,7 +2083,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                         else attention(B2, B1, a.mask, tid);
                     }
                     BAR();
-                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID, LNF>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
+                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID, LN1F>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
                 }
             }
             BAR();
@@ -2078,6 +2091,8 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
             //      split path: graph1 writes fc1's A operand split into B2[:, 0:96]; fc1 writes
             //      fc2's split A operand into B2[:, 96:288] (bytes 384..1152 of the row)
+            GFrag gb;   // graph2's fc2 bias: issued here, beside fc1's first B blocks
+            gbias_load(gb, LW + OFF_BFC2, lane);
             if constexpr (G16) {
                 const auto pre = gemm16_prefetch<G16, 12, KB32_D>(L16 + O16_FC1, wave, lane);
                 const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
@@ -2092,7 +2107,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
             } else {
                 const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
                 const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
-                if constexpr (LNF) {
+                if constexpr (LN1F) {
                     // LN1 fused into the GraphNet product's operand (partials from the O-proj epilogue)
                     if (DPK_RUN(2))
                         graph_mma<false, 0, true>(gf, XS, B1, nullptr, wave, lane, ST, LNP + l * 4 * D + 2 * D,
@@ -2108,7 +2123,12 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     gemm_wg<12, 6, E_STORE_RELU>(B1, LDX, LW + OFF_FC1, wave, lane, e, pre);
                 }
             }
-            const GFrag gf2 = gfrag_load<true>(LW + OFF_LGF, lane, LW + OFF_BFC2);   // graph2's operands, a GEMM ahead
+            GFrag gf2 = gfrag_load(LW + OFF_LGF, lane);   // graph2's operands, a GEMM ahead
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                gf2.b4[t] = gb.b4[t];
+                gf2.b1[t] = gb.b1[t];
+            }
             {
                 const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
                 if constexpr (G16) {
