@@ -325,10 +325,10 @@ __device__ __forceinline__ float sum4rows(float v) {
 // register (l>>4) at row position l&15, summed ((row0 + row2) + (row1 + row3)) like sum4rows.
 // 3 permlane swaps for 4 values instead of sum4rows' 8 (tools/rs4_probe.hip checks the map).
 __device__ __forceinline__ float rs4rows(float v0, float v1, float v2, float v3) {
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v0), "+v"(v2));
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v1), "+v"(v3));
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v0), "+v"(v2));
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v1), "+v"(v3));
     float a = v0 + v2, b = v1 + v3;
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
     return a + b;
 }
 

@@ -16,7 +16,10 @@ __device__ __forceinline__ void probe_stamp(int tag) {
     }
 }
 #define DPK_GEMM_HOOK(tag) do { __builtin_amdgcn_sched_barrier(0); probe_stamp(tag); __builtin_amdgcn_sched_barrier(0); } while (0)
-#include "../diffpose-nw_amd/csrc/dpk_kernels.hip"
+#ifndef PROBE_SRC
+#define PROBE_SRC "../diffpose-nw_amd/csrc/dpk_kernels.hip"
+#endif
+#include PROBE_SRC
 
 using namespace dpk;
 
