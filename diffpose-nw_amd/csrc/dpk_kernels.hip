@@ -1514,14 +1514,16 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
             st[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? q4[h][m & 3] : q2[h][m & 1], st[h], 0, 0, 0);
             st16[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? Q4[h][m & 3] : Q2[h][m & 1], st16[h], 0, 0, 0);
         }
-    // V operands: column tile 0 (dims 0..15) and 1 (dims 16..23; rows c >= 8 duplicate, unused)
+    // V operands: column tile 0 (dims 0..15) and 1 (dims 16..23 in rows c < 8, ones in rows
+    // c >= 8: those rows of P.V come out as the softmax denominators, below)
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
         const float* vbase = prow + h * DK + 2 * D;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             va[h][r] = vbase[(4 * g + r) * LD2 + c];
-            vb[h][r] = vbase[(4 * g + r) * LD2 + 16 + (c & 7)];
+            const float v1 = vbase[(4 * g + r) * LD2 + 16 + (c & 7)];   // unconditional load, then select
+            vb[h][r] = c < 8 ? v1 : 1.0f;
         }
         V4a[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 4 * g);
         V4b[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 16 + 4 * (g & 1));
@@ -1567,7 +1569,7 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
         mx[h] = fmaxf(max4rows(mx[h]), s_c16[h]);
         my[h] = fmaxf(max4rows(my[h]), s_1616[h]);
     }
-    float sum[NH], sum16[NH];
+    // unnormalised probabilities; the denominators come out of the P.V products (ones rows)
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
 #pragma unroll
@@ -1577,24 +1579,6 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
         }
         p16[h] = ex(s_c16[h] - mx[h]);
         u16[h] = ex(s_1616[h] - my[h]);
-        sum[h] = (p[h][0] + p[h][1]) + (p[h][2] + p[h][3]);
-        sum16[h] = (u[h][0] + u[h][1]) + (u[h][2] + u[h][3]);
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        sum[h] = sum4rows(sum[h]) + p16[h];
-        sum16[h] = sum4rows(sum16[h]) + u16[h];
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const float rs = __builtin_amdgcn_rcpf(sum[h]), rs16 = __builtin_amdgcn_rcpf(sum16[h]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            p[h][r] *= rs;
-            u[h][r] *= rs16;
-        }
-        p16[h] *= rs;
-        u16[h] *= rs16;
     }
     // ---- O^T = V^T P^T over keys 0..15 (4 MFMAs per column tile), then key 16 by FMA;
     //      query 16: this lane's keys 4g+r against V columns c and 16+c, summed over lane rows
@@ -1621,14 +1605,28 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
         ya[h] = sum4rows(ya[h]);
         yb[h] = sum4rows(yb[h]);
     }
+    // denominators: query c's over keys 0..15 sits in ob rows 8..15 (lane rows g >= 2), moved to
+    // lane rows 0,1 by one permlane32 swap; query 16's over keys 0..15 is yb of lanes c >= 8,
+    // moved to lanes c < 8 of the DPP row by a rotation by 8; key 16 added to both
+    float rs[NH], rs16[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        float sa = ob[h][0], sb = ob[h][0];
+        asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(sa), "+v"(sb));
+        const float den = (g < 2 ? sb : ob[h][0]) + p16[h];
+        const float yr = row_ror<8>(yb[h]);
+        const float den16 = (c < 8 ? yr : yb[h]) + u16[h];
+        rs[h] = __builtin_amdgcn_rcpf(den);
+        rs16[h] = __builtin_amdgcn_rcpf(den16);
+    }
     // ---- stores: O[c][h*24 + 4g..] (tile 0), O[c][h*24 + 16 + 4g..] (tile 1, g < 2);
     //      O[16][h*24 + c] and O[16][h*24 + 16 + c] (c < 8) from lane row 0
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            oa[h][r] = fmaf(p16[h], V4a[h][r], oa[h][r]);
-            ob[h][r] = fmaf(p16[h], V4b[h][r], ob[h][r]);
+            oa[h][r] = fmaf(p16[h], V4a[h][r], oa[h][r]) * rs[h];
+            ob[h][r] = fmaf(p16[h], V4b[h][r], ob[h][r]) * rs[h];
         }
         const float* v16 = prow + h * DK + 16 * LD2 + 2 * D;
         const int col = h * DK;
@@ -1637,13 +1635,13 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
             char* row16 = reinterpret_cast<char*>(orow + 16 * LDX);
             split_store4<SPLIT>(rowc, col + 4 * g, oa[h]);
             if (g < 2) split_store4<SPLIT>(rowc, col + 16 + 4 * g, ob[h]);
-            if (g == 0) split_store1<SPLIT>(row16, col + c, fmaf(u16[h], v16[c], ya[h]));
-            if (g == 1 && c < 8) split_store1<SPLIT>(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]));
+            if (g == 0) split_store1<SPLIT>(row16, col + c, fmaf(u16[h], v16[c], ya[h]) * rs16[h]);
+            if (g == 1 && c < 8) split_store1<SPLIT>(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]) * rs16[h]);
         } else {
             *reinterpret_cast<f32x4*>(orow + c * LDX + col + 4 * g) = oa[h];
             if (g < 2) *reinterpret_cast<f32x4*>(orow + c * LDX + col + 16 + 4 * g) = ob[h];
-            if (g == 0) orow[16 * LDX + col + c] = fmaf(u16[h], v16[c], ya[h]);
-            if (g == 1 && c < 8) orow[16 * LDX + col + 16 + c] = fmaf(u16[h], v16[16 + c], yb[h]);
+            if (g == 0) orow[16 * LDX + col + c] = fmaf(u16[h], v16[c], ya[h]) * rs16[h];
+            if (g == 1 && c < 8) orow[16 * LDX + col + 16 + c] = fmaf(u16[h], v16[16 + c], yb[h]) * rs16[h];
         }
     }
 }
