@@ -570,6 +570,19 @@ __device__ __forceinline__ float epi_value(float acc, float bias, float tp, floa
     else return fmaxf(v, 0.f) + tp;
 }
 
+// the same on 4 columns as packed-f32 vector ops (v_pk_add_f32); identical roundings
+template <int MODE>
+__device__ __forceinline__ f32x4 epi_value4(f32x4 acc, f32x4 bias, f32x4 tp, f32x4 old) {
+    if constexpr (MODE == E_STORE_NB) return acc;
+    const f32x4 v = acc + bias;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (MODE == E_STORE) return v;
+    else if constexpr (MODE == E_STORE_RELU) return __builtin_elementwise_max(v, z);
+    else if constexpr (MODE == E_RESID) return old + v;
+    else if constexpr (MODE == E_RESID_RELU) return old + __builtin_elementwise_max(v, z);
+    else return __builtin_elementwise_max(v, z) + tp;
+}
+
 __device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, float tcol) {
     if (e.tproj_pose_stride == 0) return tcol;
     const int pose = min(e.pose0 + row / J, e.pose_max);
@@ -787,10 +800,7 @@ __device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* 
         for (int c = 0; c < NCW; ++c) {
             const int col4 = gcol[c] * 16 + kq;
             const f32x4 tp = tproj4(row, col4, tp4[c]);
-            f32x4 v;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                v[r] = epi_value<MODE>(g.acc[i][c][r], bias4[c][r], tp[r], RES ? old[i][c][r] : 0.f);
+            const f32x4 v = epi_value4<MODE>(g.acc[i][c], bias4[c], tp, RES ? old[i][c] : f32x4{0.f, 0.f, 0.f, 0.f});
             *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
             vo[c] = v;
         }
@@ -1623,11 +1633,9 @@ __device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsi
     //      O[16][h*24 + c] and O[16][h*24 + 16 + c] (c < 8) from lane row 0
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            oa[h][r] = fmaf(p16[h], V4a[h][r], oa[h][r]) * rs[h];
-            ob[h][r] = fmaf(p16[h], V4b[h][r], ob[h][r]) * rs[h];
-        }
+        const f32x4 p4 = {p16[h], p16[h], p16[h], p16[h]};
+        oa[h] = __builtin_elementwise_fma(p4, V4a[h], oa[h]) * rs[h];
+        ob[h] = __builtin_elementwise_fma(p4, V4b[h], ob[h]) * rs[h];
         const float* v16 = prow + h * DK + 16 * LD2 + 2 * D;
         const int col = h * DK;
         if constexpr (SPLIT) {
