@@ -1803,7 +1803,7 @@ __device__ __forceinline__ void graph_op(const float* __restrict__ L, const floa
 struct GFrag {
     float lb[5], l16[5];
     f32x4 b4[6];
-    float b1[6];
+    float b1[2];    // joint-16 row: bias of column cl of tiles g and 4 + (g & 1) (graph_mma's map)
 };
 template <bool BIAS = false>
 __device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int lane,
@@ -1828,10 +1828,9 @@ __device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int la
 __device__ __forceinline__ void gbias_load(GFrag& f, const float* __restrict__ bias, int lane) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
-        f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
-        f.b1[t] = bias[16 * t + cl];
-    }
+    for (int t = 0; t < 6; ++t) f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
+    f.b1[0] = bias[16 * g + cl];
+    f.b1[1] = bias[16 * (4 + (g & 1)) + cl];
 }
 
 // LNA: src is raw x; the operand is LayerNorm(x) formed in registers (fused LN1: statistics
@@ -1848,15 +1847,17 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
     const float(&l16)[5] = f.l16;
     const float* xp = src + wave * J * LDX + cl;
     const int row_j = wave * J + cl, row16 = wave * J + 16;
+    // joint 16's output row: lane row g ends with column cl of tiles g and 4 + (g & 1)
+    // (reduce-scatter below); rows 2, 3 hold a duplicate of the second and store nothing
+    const int c16a = 16 * g + cl, c16b = 16 * (4 + (g & 1)) + cl;
     // RESID: the residual rows this lane updates, read before the MFMAs (dst != src)
     f32x4 old[6];
-    float old16[6];
+    float old16a = 0.f, old16b = 0.f;
     if constexpr (RESID) {
 #pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            old[t] = *reinterpret_cast<const f32x4*>(dst + row_j * LDX + 16 * t + 4 * g);
-            old16[t] = dst[row16 * LDX + 16 * t + cl];
-        }
+        for (int t = 0; t < 6; ++t) old[t] = *reinterpret_cast<const f32x4*>(dst + row_j * LDX + 16 * t + 4 * g);
+        old16a = dst[row16 * LDX + c16a];
+        old16b = dst[row16 * LDX + c16b];
     }
     float a[6][5];
 #pragma unroll
@@ -1902,21 +1903,19 @@ __device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, floa
             *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = acc[t];
         }
     }
-    float v16[6];
-#pragma unroll
-    for (int t = 0; t < 6; ++t) v16[t] = sum4rows(p16[t]);
-    if (g == 0) {
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            const int c = 16 * t + cl;
-            if constexpr (SPLIT_OUT) {
-                split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c, v16[t]);
-            } else if constexpr (RESID) {
-                dst[row16 * LDX + c] = old16[t] + (v16[t] + f.b1[t]);
-            } else {
-                dst[row16 * LDX + c] = v16[t];
-            }
-        }
+    // joint 16: the per-lane partial sums reduce-scattered over the 4 lane rows (rs4rows: lane
+    // row g gets register g's total; same summation order as sum4rows), 6 permlanes for 6 tiles
+    const float va = rs4rows(p16[0], p16[1], p16[2], p16[3]);    // tile g
+    const float vb = rs4rows(p16[4], p16[5], p16[4], p16[5]);    // tile 4 + (g & 1)
+    if constexpr (SPLIT_OUT) {
+        split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c16a, va);
+        if (g < 2) split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c16b, vb);
+    } else if constexpr (RESID) {
+        dst[row16 * LDX + c16a] = old16a + (va + f.b1[0]);
+        if (g < 2) dst[row16 * LDX + c16b] = old16b + (vb + f.b1[1]);
+    } else {
+        dst[row16 * LDX + c16a] = va;
+        if (g < 2) dst[row16 * LDX + c16b] = vb;
     }
 }
 
