@@ -7,25 +7,36 @@ human36m_diffpose_uvxyz_cpn eval, H=1), inputs already resident in HBM, plus —
 N>1 — the RCCL all-gather of the final poses to every rank (frame-sharded, weak
 scaling).  `value` is whole-job poses/s = frames processed by all ranks / time.
 
+Launch:
+  python bench.py [--gpus N --steps K --warmup W]      N>1: spawns N ranks itself (one process per
+                                                         GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set
+                                                         before any HIP call; the parent never touches
+                                                         the GPU) and exits non-zero if any rank fails
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  python bench.py --config 3|4|5                        the other BASELINE configs (presets below)
+  python bench.py --gpus 2 --cpu-dry                    launcher/sharding/all-gather rehearsal on CPU
+                                                         (gloo, an elementwise stub instead of the
+                                                         sampler; no GPU, nothing timed is meaningful)
+
 Also reported on the same JSON line:
   roofline      the sampler kernel's algorithmic FLOP rate (25,996,254 FLOP per
                 pose-step × poses × K ÷ its average launch duration, measured with HIP events
                 around that kernel on the stream it is launched on) vs the fp32 MFMA peak;
   cpu_baseline  the golden-pinned oracle (torch CPU, the reference's op sequence) timed on
                 this host's cores on the first --cpu-frames frames of the same batch (rank 0,
-                N=1 only);
+                N=1 only), best of --cpu-repeats after a warm-up call, at the host threads the
+                job is allotted (OMP_NUM_THREADS; --cpu-threads adds legs);
   parity        MPJPE (mm) of the HIP result vs the oracle on those frames, and max |diff|;
   variants      the same measurement (warmup, timed steps, roofline, parity) in the other GEMM
                 modes: the headline is fp32 MFMA (the reference's arithmetic); "f16x3" runs the
                 layer GEMMs as three fp16-split MFMA products with fp32 accumulation; "bf16"
                 rounds their operands to bf16 (BASELINE config 3's tolerance study).
-
-  python bench.py [--gpus N --steps K --warmup W]
-  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,27 +53,111 @@ DTYPES = {"fp32": "fp32",
           "bf16": "bf16 layer GEMMs (fp32 accumulate; LN/attention/graph/DDIM fp32): tolerance study"}
 METRIC = "poses/sec (B=1024, 17j, K=50 DDIM) at 1/2/4/8 MI355X; MPJPE Δ vs ref"
 
+# BASELINE.json configs 2-5 (config 1 is the reference's own CPU case, timed as cpu_baseline).
+# frames: per GPU (weak scaling) unless total_frames is set (fixed job, strong scaling).
+CONFIGS = {
+    2: dict(yml="human36m_diffpose_uvxyz_cpn", frames=1024, total_frames=None, hyp=1, K=50, T_test=50, T=51,
+            gemm="fp32", graph=False),
+    3: dict(yml="human36m_diffpose_uvxyz_gt", frames=1024, total_frames=None, hyp=1, K=100, T_test=100, T=101,
+            gemm="bf16", graph=False),
+    4: dict(yml="human36m_diffpose_uvxyz_cpn", frames=1024, total_frames=None, hyp=1, K=50, T_test=50, T=51,
+            gemm="fp32", graph=False),
+    5: dict(yml="human36m_diffpose_uvxyz_cpn", frames=None, total_frames=1024, hyp=20, K=50, T_test=50, T=51,
+            gemm="fp32", graph=True),
+}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames", type=int, default=1024, help="frames per GPU")
-    ap.add_argument("--hyp", type=int, default=1, help="hypotheses per frame (test_times)")
-    ap.add_argument("--K", type=int, default=50, help="DDIM steps (test_timesteps)")
-    ap.add_argument("--T-test", type=int, default=50, help="test_num_diffusion_timesteps")
-    ap.add_argument("--T", type=int, default=51, help="diffusion.num_diffusion_timesteps")
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=2,
+                    help="BASELINE.json config preset (2: cpn B=1024 K=50 fp32, the headline; 3: gt K=100 bf16; "
+                         "4: cpn 1024 frames per GPU; 5: cpn 1024 frames x H=20 split over the GPUs, hipGraph)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (overrides the preset)")
+    ap.add_argument("--total-frames", type=int, default=None,
+                    help="frames of the whole job, split over the GPUs (strong scaling; overrides --frames)")
+    ap.add_argument("--hyp", type=int, default=None, help="hypotheses per frame (test_times)")
+    ap.add_argument("--K", type=int, default=None, help="DDIM steps (test_timesteps)")
+    ap.add_argument("--T-test", type=int, default=None, help="test_num_diffusion_timesteps")
+    ap.add_argument("--T", type=int, default=None, help="diffusion.num_diffusion_timesteps")
     ap.add_argument("--eta", type=float, default=0.0)
-    ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
-    ap.add_argument("--cpu-frames", type=int, default=1024)
-    ap.add_argument("--cpu-repeats", type=int, default=1)
+    ap.add_argument("--graph", action="store_true", default=None, help="replay the step from a captured hipGraph")
+    ap.add_argument("--cpu-frames", type=int, default=128)
+    ap.add_argument("--cpu-repeats", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=str, default=None,
+                    help="comma-separated thread counts for the CPU baseline legs (default: the box's CPU share, "
+                         "OMP_NUM_THREADS, or every physical core of this process's affinity when unset)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--gemm", choices=("fp32", "f16x3", "bf16"), default="fp32",
+    ap.add_argument("--gemm", choices=("fp32", "f16x3", "bf16"), default=None,
                     help="per-layer GEMM arithmetic of the headline (dpk_set_gemm_mode); fp32 is the reference's")
     ap.add_argument("--no-variants", dest="variants", action="store_false",
                     help="skip timing the other GEMM mode (reported under 'variants')")
-    return ap.parse_args()
+    ap.add_argument("--cpu-dry", action="store_true",
+                    help="rehearse the multi-rank launch, sharding and all-gather on CPU (gloo) with an "
+                         "elementwise stub in place of the HIP sampler")
+    args = ap.parse_args(argv)
+    preset = CONFIGS[args.config]
+    for k in ("hyp", "K", "T_test", "T", "gemm", "graph"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
+    if args.frames is None and args.total_frames is None:
+        args.frames, args.total_frames = preset["frames"], preset["total_frames"]
+    args.yml = preset["yml"]
+    return args
+
+
+def frames_layout(args, world):
+    """(total frames of the job, scaling kind)."""
+    if args.total_frames is not None:
+        return args.total_frames, "strong"
+    return args.frames * world, "weak"
+
+
+# ---------------------------------------------------------------------------------------------
+# launcher: N ranks from a plain `python bench.py --gpus N` (no torch import, no HIP call here)
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv) -> int:
+    """Start n rank processes of this script with the torch.distributed.run environment and wait
+    for all of them.  Returns 0 only if every rank exited 0; when one fails the others are
+    terminated (by their own PIDs) and its code is returned."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DPK_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
 
 
 def host_cpu_model():
@@ -75,6 +170,18 @@ def host_cpu_model():
     return "unknown"
 
 
+def physical_cores(cpus):
+    """Number of distinct (package, core) pairs among the logical CPUs ``cpus`` (SMT siblings once)."""
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            seen.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            return len(cpus)
+    return len(seen) or len(cpus)
+
+
 def mpjpe_mm(out_uvxyz, targets, hyp):
     import numpy as np
 
@@ -83,90 +190,176 @@ def mpjpe_mm(out_uvxyz, targets, hyp):
     return float(np.mean(np.linalg.norm(xyz - np.asarray(targets, np.float64), axis=-1)) * 1000.0)
 
 
-def main():
-    args = parse()
+def cpu_baseline(args, x_all, seq, betas, K, hyp):
+    """The oracle (reference op sequence, torch CPU fp32) on the first cpu_frames frames, best of
+    cpu_repeats, at the host thread count this job is allotted (SURVEY §8d asks for all physical
+    cores; the GPU box allots 16 CPUs per GPU through OMP_NUM_THREADS and asks that worker pools stay
+    within that share, so the share is the default leg; --cpu-threads adds others).
+    Returns (result dict, final poses of the share run, frames timed)."""
+    import numpy as np
+    import torch
+
+    from diffpose_amd.data import repeat_hypotheses
+    from diffpose_amd.weights import synthetic_state_dict
+    from oracle import gcndiff_oracle as O
+
+    cpus = sorted(os.sched_getaffinity(0))
+    phys = physical_cores(cpus)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or phys
+    share = max(1, min(share, len(cpus)))
+    n_cpu = min(args.cpu_frames, x_all.shape[0])
+    xc = torch.from_numpy(repeat_hypotheses(x_all[:n_cpu], hyp))
+    P = O.params_to_torch(synthetic_state_dict())
+    adj = O.adjacency()
+    mask = torch.ones(1, 1, 17, dtype=torch.bool)
+
+    def run(x):
+        xs, _ = O.generalized_steps(x, mask, seq, lambda a, m, t: O.gcndiff_forward(P, adj, a, m, t), betas, eta=0.0)
+        return xs[-1]
+
+    legs, ref = {}, None
+    legs_wanted = {share}
+    if args.cpu_threads:
+        legs_wanted |= {max(1, min(int(t), len(cpus))) for t in args.cpu_threads.split(",") if t.strip()}
+    for threads in sorted(legs_wanted):
+        torch.set_num_threads(threads)
+        run(xc[: min(8, xc.shape[0])])                     # thread pool + allocator warm-up, untimed
+        times = []
+        for _ in range(max(1, args.cpu_repeats)):
+            t0 = time.perf_counter()
+            out = run(xc)
+            times.append(time.perf_counter() - t0)
+        legs[threads] = (n_cpu / min(times), times)
+        if threads == share:
+            ref = out
+    best_threads = max(legs, key=lambda t: legs[t][0])
+    v, times = legs[best_threads]
+    res = {
+        "value": round(v, 3), "unit": "poses/s", "cores": best_threads, "kind": "port",
+        "sample": (f"oracle generalized_steps+GCNdiff (torch CPU fp32, reference op order, golden-pinned) on the "
+                   f"first {n_cpu} frames x H={hyp} of the same batch, K={K}, best of {max(1, args.cpu_repeats)} "
+                   f"after an untimed warm-up call; host '{host_cpu_model()}', {len(cpus)} logical CPUs in this "
+                   f"process's affinity ({phys} physical cores); " +
+                   "; ".join(f"{t} threads: {legs[t][0]:.1f} poses/s (runs {', '.join(f'{s:.2f}' for s in legs[t][1])} s)"
+                             for t in sorted(legs))),
+        "by_threads": {str(t): round(legs[t][0], 3) for t in sorted(legs)},
+    }
+    torch.set_num_threads(share)
+    return res, (ref.numpy() if ref is not None else None), n_cpu
+
+
+# ---------------------------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------------------------
+def rank_main(args):
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from diffpose_amd import dist as D
     from diffpose_amd.data import repeat_hypotheses, shard_frames, synthetic_batch
-    from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
     from diffpose_amd.schedule import get_beta_schedule, make_seq
-    from diffpose_amd.weights import synthetic_state_dict
 
     rank, world, local = D.world_info()
+    launched = "RANK" in os.environ and "MASTER_ADDR" in os.environ
     if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    # under a launcher (torch.distributed.run sets RANK/MASTER_ADDR) the RCCL path runs at every
-    # N, N=1 included, so per-GPU work is the same at every point of the scaling sweep
-    use_dist = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a different world size",
+              file=sys.stderr)
+        return 2
+    dry = args.cpu_dry
+    if dry:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    # under a launcher (ours or torch.distributed.run) the collective path runs at every N, N=1 included,
+    # so per-GPU work is the same at every point of the scaling sweep
+    use_dist = world > 1 or launched
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        if dry:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
-    # ---- model, schedule, inputs (synthetic, seeded) ----
-    model = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
-    model.load_state_dict(synthetic_state_dict())
+    def sync():
+        if not dry:
+            torch.cuda.synchronize(dev)
+
+    # ---- schedule, inputs (synthetic, seeded), model ----
     seq = make_seq("uniform", args.T_test, args.K)
     betas = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
                                                num_diffusion_timesteps=args.T)).float()
-    model.set_schedule(seq, betas, args.eta)
     K = len(seq)
-    B_total = args.frames * world
+    B_total, scaling = frames_layout(args, world)
     x_all, tgt_all = synthetic_batch(B_total)
     lo, hi = shard_frames(B_total, world, rank)
     x_host = repeat_hypotheses(x_all[lo:hi], args.hyp)
     x = torch.from_numpy(x_host).to(dev)
     out = torch.empty_like(x)
     rows = x.shape[0]
+    model = None
+    if not dry:
+        from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
+        from diffpose_amd.weights import synthetic_state_dict
+
+        model = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
+        model.load_state_dict(synthetic_state_dict())
+        model.set_schedule(seq, betas, args.eta)
+
+    gathered = {}
 
     def step():
-        model.sample(x, seq, betas, eta=args.eta, out=out)
-        if use_dist:                             # the one data-path collective: final poses to every rank
-            D.gather_frames(out, B_total, args.hyp)
+        if dry:
+            torch.mul(x, 2.0, out=out)                 # stand-in for the sampler: rank-independent, exact
+        else:
+            model.sample(x, seq, betas, eta=args.eta, out=out)
+        if use_dist:                                   # the one data-path collective: final poses to every rank
+            gathered["all"] = D.gather_frames(out, B_total, args.hyp)
 
     def measure(gemm):
         """Time exactly args.steps steps (barrier + sync both sides, max over ranks) in one GEMM mode."""
-        model.set_gemm_mode(gemm)
+        if model is not None:
+            model.set_gemm_mode(gemm)
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize()
+        sync()
         graph = None
-        if args.graph:
+        if args.graph and not dry:
             graph = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
-                step()                                   # warm the side stream
+                step()                                 # warm the side stream
             torch.cuda.current_stream(dev).wait_stream(s)
-            torch.cuda.synchronize()
+            sync()
             with torch.cuda.graph(graph):
                 step()
             run = graph.replay
         else:
             run = step
-            model.profile(True)
+            if model is not None:
+                model.profile(True)
         if use_dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             run()
-        torch.cuda.synchronize()
+        sync()
         if use_dist:
             dist.barrier()
-        elapsed = D.max_over_ranks(time.perf_counter() - t0, device=dev)
-        kernel_ms = model.kernel_times_ms() if graph is None else []
-        model.profile(False)
-        return elapsed, kernel_ms
+        mine = time.perf_counter() - t0
+        elapsed = D.max_over_ranks(mine, device=dev)
+        kernel_ms = model.kernel_times_ms() if (graph is None and model is not None) else []
+        if model is not None:
+            model.profile(False)
+        return elapsed, mine, kernel_ms
 
     def roofline(gemm, kernel_ms):
         if not kernel_ms:
             return None
-        avg_kernel_ms = float(np.mean(kernel_ms))
+        km = np.asarray(kernel_ms, dtype=np.float64)
+        avg_kernel_ms = float(km.mean())
         achieved = W_ALG * rows * K / (avg_kernel_ms * 1e-3) / 1e12
         # f16x3: every fp32 product is three f16 MFMA passes, so the fp32-equivalent peak is 1/3 of f16's;
         # bf16: one pass at the dense bf16 peak (same rate as f16)
@@ -174,14 +367,15 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
                 "kernel": "dpk::sample_kernel<0, *, %d>" % {"fp32": 0, "f16x3": 1, "bf16": 2}[gemm],
-                "avg_launch_ms": round(avg_kernel_ms, 4),
+                "avg_launch_ms": round(avg_kernel_ms, 4), "median_launch_ms": round(float(np.median(km)), 4),
+                "min_launch_ms": round(float(km.min()), 4),
                 "launches": len(kernel_ms), "flop_per_launch": W_ALG * rows * K,
                 "per_unit": f"{W_ALG} FLOP per pose-step (SURVEY 8d) x {rows} poses x {K} steps"}
         tfile = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tfile):
             try:
                 tr = json.load(open(tfile))
-                key = f"frames{args.frames}_hyp{args.hyp}_K{K}" + ("" if gemm == "fp32" else "_" + gemm)
+                key = f"rows{rows}_K{K}" + ("" if gemm == "fp32" else "_" + gemm)
                 if key in tr:
                     roof["traffic"] = tr[key]["hbm_bytes_per_launch"]
                     roof["traffic_source"] = tr[key]["source"]
@@ -190,14 +384,40 @@ def main():
         return roof
 
     # ---- timed region (headline mode), then the other GEMM mode as a variant on the same line ----
-    elapsed, kernel_ms = measure(args.gemm)
-    out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0) else None
+    elapsed, mine, kernel_ms = measure(args.gemm)
+    per_rank_ms = [mine / args.steps * 1e3]
+    allgather_ms = None
+    reassembly = None
+    if use_dist:
+        t = torch.tensor([mine / args.steps * 1e3], dtype=torch.float64, device=dev)
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        per_rank_ms = [round(float(v.item()), 4) for v in lst]
+        # the all-gather alone, same barrier/sync bracket, max over ranks
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        n_ag = 20
+        for _ in range(n_ag):
+            full = D.gather_frames(out, B_total, args.hyp)
+        sync()
+        dist.barrier()
+        allgather_ms = D.max_over_ranks(time.perf_counter() - t0, device=dev) / n_ag * 1e3
+        if dry:   # the stub is exact, so the reassembled batch must equal the stub over the whole batch
+            expect = torch.from_numpy(repeat_hypotheses(x_all, args.hyp)) * 2.0
+            reassembly = bool(torch.equal(full.cpu(), expect))
+        else:     # every rank's own shard must sit where shard_rows says it belongs
+            idx = D.shard_rows(B_total, args.hyp, world, rank).to(dev)
+            ok = torch.tensor([1 if torch.equal(full[idx], out) else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            reassembly = bool(ok.item())
+    out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0 and not dry) else None
     variants = {}
-    if args.variants:
+    if args.variants and not dry:
         for g in ("fp32", "f16x3"):
             if g == args.gemm:
                 continue
-            e2, k2 = measure(g)
+            e2, _, k2 = measure(g)
             variants[g] = {"value": round(B_total * args.steps / e2, 2), "ms_per_step": round(e2 / args.steps * 1e3, 4),
                            "roofline": roofline(g, k2),
                            "dtype": DTYPES[g]}
@@ -212,52 +432,39 @@ def main():
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None,
         "dtype": DTYPES[args.gemm],
         "data": "synthetic: seeded PCG64 Human3.6M-shaped uvxyz poses and GCNdiff weights (no H36M/checkpoints offline)",
-        "config": {"workload": f"human36m_diffpose_uvxyz_cpn eval: {args.frames} frames/GPU x H={args.hyp}, "
-                               f"K={K} DDIM (uniform skip over T'={args.T_test}, T={args.T}), eta={args.eta}",
-                   "frames_per_gpu": args.frames, "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
+        "config": {"workload": f"BASELINE config {args.config}: {args.yml} eval, {B_total} frames x H={args.hyp} "
+                               f"({rows} rows on rank 0), K={K} DDIM (uniform skip over T'={args.T_test}, "
+                               f"T={args.T}), eta={args.eta}",
+                   "baseline_config": args.config, "frames_total": B_total, "frames_per_gpu": hi - lo,
+                   "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
                    "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if use_dist else ""),
                    "hipgraph": bool(args.graph), "gemm": args.gemm},
+        "per_rank_ms": per_rank_ms,
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if dry:
+        result.update({"dtype": "fp32", "data": "cpu-dry rehearsal: elementwise stub instead of the sampler",
+                       "value": None, "roofline": None})
+        result["config"]["parallelism"] = f"dp{world} frame-sharded + gloo all_gather (cpu-dry)"
+    if allgather_ms is not None:
+        result["allgather_ms"] = round(allgather_ms, 4)
+        result["reassembly_ok"] = reassembly
     if variants:
         result["variants"] = variants
-    if args.hyp > 1:
+    if args.hyp > 1 and value is not None:
         result["rows_per_s"] = round(value * args.hyp, 2)
 
     # ---- CPU baseline + parity (rank 0, N=1) ----
-    if world == 1 and rank == 0 and not args.no_cpu:
-        from oracle import gcndiff_oracle as O
-
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        cores = max(1, min(cores, os.cpu_count() or cores))
-        torch.set_num_threads(cores)
-        n_cpu = min(args.cpu_frames, args.frames)
-        xc = torch.from_numpy(repeat_hypotheses(x_all[:n_cpu], args.hyp))
-        P = O.params_to_torch(synthetic_state_dict())
-        adj = O.adjacency()
-        mask = torch.ones(1, 1, 17, dtype=torch.bool)
-        best, ref = None, None
-        for _ in range(max(1, args.cpu_repeats)):
-            t0 = time.perf_counter()
-            xs, _ = O.generalized_steps(xc, mask, seq, lambda a, m, t: O.gcndiff_forward(P, adj, a, m, t), betas,
-                                        eta=0.0)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-            ref = xs[-1]
-        result["cpu_baseline"] = {
-            "value": round(n_cpu / best, 3), "unit": "poses/s", "cores": cores, "kind": "port",
-            "sample": f"oracle generalized_steps+GCNdiff (torch CPU fp32, reference op order, golden-pinned) on the "
-                      f"first {n_cpu} frames x H={args.hyp} of the same batch, K={K}, best of "
-                      f"{max(1, args.cpu_repeats)}: {best:.2f} s; host '{host_cpu_model()}', "
-                      f"{os.cpu_count()} logical CPUs, {cores} threads"}
-        if args.eta == 0.0:
-            idx = np.concatenate([np.arange(h * args.frames, h * args.frames + n_cpu) for h in range(args.hyp)])
-            ref_np = ref.numpy()
+    if world == 1 and rank == 0 and not args.no_cpu and not dry:
+        cb, ref_np, n_cpu = cpu_baseline(args, x_all, seq, betas, K, args.hyp)
+        result["cpu_baseline"] = cb
+        if args.eta == 0.0 and ref_np is not None:
+            idx = np.concatenate([np.arange(h * (hi - lo), h * (hi - lo) + n_cpu) for h in range(args.hyp)])
             tg = tgt_all[:n_cpu]
             m_r = mpjpe_mm(ref_np, tg, args.hyp)
 
@@ -281,7 +488,19 @@ def main():
         print(json.dumps(result), flush=True)
     if use_dist:
         dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if args.gpus > 1 and "RANK" not in os.environ:
+        return launch(args.gpus, argv)
+    return rank_main(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

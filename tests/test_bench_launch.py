@@ -1,0 +1,47 @@
+"""CPU: `python bench.py --gpus N` starts N ranks itself (verdict r01 item 1), reports
+n_gpus = N and reassembles the frame-sharded batch through the all-gather, using the
+--cpu-dry rehearsal (gloo, an elementwise stub in place of the HIP sampler — no oracle, no GPU).
+The reference runs one DataParallel replica (runners/diffpose_frame.py:126-127); this is the
+launcher for the frame-sharded replacement."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                          "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+@pytest.mark.parametrize("extra,scaling,frames_total", [
+    (["--frames", "8"], "weak", 16),                        # config 2/4 shape: frames per GPU
+    (["--config", "5", "--total-frames", "7"], "strong", 7),  # config 5 shape: ragged split, H=20
+])
+def test_bench_spawns_ranks_and_reassembles(extra, scaling, frames_total):
+    rc, line, err = _run(["--gpus", "2", "--cpu-dry", "--steps", "2", "--warmup", "1"] + extra)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2
+    assert line["scaling"] == scaling
+    assert line["config"]["frames_total"] == frames_total
+    assert line["reassembly_ok"] is True
+    assert len(line["per_rank_ms"]) == 2
+    assert line["allgather_ms"] > 0
+
+
+def test_bench_refuses_world_size_mismatch():
+    # a launcher that started 1 rank for --gpus 2 must not produce a line claiming 2 GPUs
+    rc, line, err = _run(["--gpus", "2", "--cpu-dry", "--steps", "1", "--warmup", "0", "--frames", "4"],
+                         env_extra={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    assert rc != 0
+    assert line is None
+    assert "WORLD_SIZE" in err
