@@ -260,6 +260,7 @@ struct SampleArgs {
     float eta;
     unsigned long long seed;
     int phase_delay;      // two workgroups per CU: start delay (cycles) of the grid's second half
+    int num_layers;       // GraAttenLayer + _ResChebGC_diff pairs run (config num_layer, 1..NL)
 #if DPK_TRACE
     unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
     int trace_step;
@@ -2045,7 +2046,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
         BAR();
 
 #pragma unroll 1
-        for (int l = 0; l < NL; ++l) {
+        for (int l = 0; l < a.num_layers; ++l) {
             const float* LW = W + l * LAYER_FLOATS;
             const char* L16 = arena16 + (size_t)l * LAYER16_BYTES;
             char* B1b = reinterpret_cast<char*>(B1);
@@ -2185,7 +2186,7 @@ __global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, con
                     if (DPK_RUN(4)) cheb_prep<SPARSE, 0, true>(CW, B1, B2, wave, lane);
                     BAR();
                     if constexpr (LNF)
-                        if (l + 1 < NL) qpre = gemm_prefetch<18, 6>(LW + LAYER_FLOATS + OFF_QKV, wave, lane);
+                        if (l + 1 < a.num_layers) qpre = gemm_prefetch<18, 6>(LW + LAYER_FLOATS + OFF_QKV, wave, lane);
                     if (DPK_RUN(16 | 1024))
                         gemm_wg<6, 18, E_RESID_RELU, LNF, false, true>(B2, LD2, LW + OFF_C2, wave, lane, e, pre,
                                                                        ST, nullptr, nullptr, B1, LDX);
@@ -2347,23 +2348,46 @@ __global__ void __launch_bounds__(256) ddim_kernel(const float* __restrict__ xt,
 // =======================================================================================
 using namespace dpk;
 
+// One DDIM schedule on the device, immutable once built: the step scalars coef [K][6] and the
+// per-step timestep projections tps [K][NL][D] = temb_proj_l(swish(temb(t_s))) (they depend only
+// on the weights and the schedule; SURVEY a7: batch-invariant).  dpk_set_schedule builds a new one
+// instead of rewriting the old, so a launch still in flight (or a captured graph) keeps reading
+// the schedule it was launched with; the old one is freed once every stream that used it has
+// passed its last launch (an event per stream), or never if a graph was captured with it.
+struct Sched {
+    float* buf = nullptr;          // device: coef, then tps (16-byte aligned)
+    float* coef = nullptr;
+    float* tps = nullptr;
+    int K = 0;
+    float eta = 0.f;
+    std::vector<float> h_coef;
+    uint64_t tps_gen = 0;          // weights generation tps was computed from (0: not yet)
+    bool pinned = false;           // read by a captured graph: kept until dpk_destroy
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;   // last launch on each stream
+};
+
+// dpk_eps's per-pose projections [N][NL][D], one buffer per caller stream: two dpk_eps calls on
+// different streams never share one, and calls on the same stream are ordered by the stream
+struct EpsBuf {
+    hipStream_t st = nullptr;
+    float* p = nullptr;
+    int cap = 0;
+};
+
 struct dpk_handle {
     int device = 0;
     int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
+    int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int phase_delay = 0;           // DPK_PHASE_DELAY (cycles), two-workgroups-per-CU builds only
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
-    float* coef = nullptr;         // device: [K][6]
-    float* tproj = nullptr;        // device: [cap][NL][D]
-    int tproj_cap = 0;
-    // dpk_sample's per-step temb projections [K][NL][D]: depend only on the weights and the
-    // schedule, so they are computed on the first dpk_sample after either changes and reused
-    float* tps = nullptr;
-    int tps_cap = 0;
-    bool tps_valid = false;
-    hipEvent_t tps_ev = nullptr;   // recorded after the temb launch (other streams wait on it)
-    hipStream_t tps_stream = nullptr;
+    float* tproj_zero = nullptr;   // device: [NL][D] zeros (GCNpose: no timestep projection)
+    hipStream_t aux = nullptr;     // handle-internal stream for schedule construction
+    uint64_t weights_gen = 0;      // bumped by every weight/graph upload
+    Sched* sched = nullptr;        // current schedule
+    std::vector<Sched*> retired;   // replaced schedules not yet known to be unused
+    std::vector<EpsBuf> eps_bufs;
     std::vector<float> h_arena;    // host staging of the arena
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
@@ -2372,10 +2396,7 @@ struct dpk_handle {
     int gemm_mode = 0;             // 0: fp32 MFMA, 1: 3x fp16-split MFMA, 2: bf16 MFMA (dpk_set_gemm_mode)
     bool w16_ok = true;            // loaded weights fit the split-fp16 packing (|w| < 1015)
     std::vector<float> h_temb;
-    bool have_graph = false, have_weights = false, have_sched = false;
-    std::vector<float> h_coef;
-    int K = 0;
-    float eta = 0.f;
+    bool have_graph = false, have_weights = false;
     unsigned mask = (1u << J) - 1u;
     std::vector<float> h_adj;
     bool profiling = false;
@@ -2506,17 +2527,65 @@ static void graph_lap(const float* A, float* Lg) {
         for (int j = 0; j < J; ++j) Lg[i * J + j] = (dh[i] * A[i * J + j]) * dh[j];
 }
 
-static int ensure_tproj(dpk_handle* h, int slots) {
-    if (h->tproj_cap >= slots) return DPK_OK;
-    if (h->tproj) HIPCHK(h, hipFree(h->tproj));
-    h->tproj = nullptr;
-    HIPCHK(h, hipMalloc(&h->tproj, (size_t)slots * NL * D * 4));
-    h->tproj_cap = slots;
+// Is `st` capturing a graph right now?  (Launches then become graph nodes: nothing may be
+// allocated or freed, and the schedule they read must outlive the graph.)
+static int capturing(dpk_handle* h, hipStream_t st, bool* cap) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(h, hipStreamIsCapturing(st, &cs));
+    *cap = cs != hipStreamCaptureStatusNone;
+    return DPK_OK;
+}
+
+static void sched_free(Sched* s) {
+    if (s->buf) (void)hipFree(s->buf);
+    for (auto& u : s->uses) (void)hipEventDestroy(u.second);
+    delete s;
+}
+
+// Free the retired schedules whose every recorded use has completed (never the pinned ones).
+static void sched_sweep(dpk_handle* h) {
+    std::vector<Sched*> keep;
+    for (Sched* s : h->retired) {
+        bool done = !s->pinned;
+        for (auto& u : s->uses) done = done && hipEventQuery(u.second) == hipSuccess;
+        if (done) sched_free(s);
+        else keep.push_back(s);
+    }
+    h->retired.swap(keep);
+}
+
+// After enqueuing a launch that reads `s` on `st`: pin it if the launch was captured, else
+// record its completion on that stream.
+static int sched_note_use(dpk_handle* h, Sched* s, hipStream_t st, bool cap) {
+    if (cap) {
+        s->pinned = true;
+        return DPK_OK;
+    }
+    hipEvent_t ev = nullptr;
+    for (auto& u : s->uses)
+        if (u.first == st) ev = u.second;
+    if (!ev) {
+        HIPCHK(h, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        s->uses.push_back({st, ev});
+    }
+    HIPCHK(h, hipEventRecord(ev, st));
+    return DPK_OK;
+}
+
+// tps of `s` from the current weights, on the handle's own stream; returns once they are written
+static int sched_compute_tps(dpk_handle* h, Sched* s) {
+    hipLaunchKernelGGL(temb_kernel, dim3(s->K), dim3(256), 0, h->aux, h->temb, s->coef + 5, 6, s->tps);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->aux));
+    s->tps_gen = h->weights_gen;
     return DPK_OK;
 }
 
 static int upload(dpk_handle* h) {
     HIPCHK(h, hipSetDevice(h->device));
+    // launches already enqueued on any stream may still read the arena: overwrite it only after
+    // the device has drained (weights and graphs are loaded rarely; the launches stay async)
+    HIPCHK(h, hipDeviceSynchronize());
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
     if (!h->arena16) HIPCHK(h, hipMalloc(&h->arena16, (size_t)ARENA16_BYTES));
     HIPCHK(h, hipMemcpy(h->arena16, h->h_arena16.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
@@ -2525,6 +2594,17 @@ static int upload(dpk_handle* h) {
     if (!h->temb) HIPCHK(h, hipMalloc(&h->temb, (size_t)TEMB_FLOATS * 4));
     HIPCHK(h, hipMemcpy(h->arena, h->h_arena.data(), (size_t)ARENA_FLOATS * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->temb, h->h_temb.data(), (size_t)TEMB_FLOATS * 4, hipMemcpyHostToDevice));
+    ++h->weights_gen;
+    if (!h->have_weights || h->kind != 0) return DPK_OK;
+    // every live schedule (current, retired, pinned by a graph) follows the new weights
+    if (h->sched) {
+        const int rc = sched_compute_tps(h, h->sched);
+        if (rc) return rc;
+    }
+    for (Sched* s : h->retired) {
+        const int rc = sched_compute_tps(h, s);
+        if (rc) return rc;
+    }
     return DPK_OK;
 }
 
@@ -2558,7 +2638,7 @@ int dpk_kernel_geometry(int* ppw, int* tpw, int* lds) {
 int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (!cfg || !out) return DPK_E_INVALID;
     *out = nullptr;
-    if (cfg->hid_dim != D || cfg->num_layers != NL || cfg->n_head != NH || cfg->n_pts != J)
+    if (cfg->hid_dim != D || cfg->num_layers < 1 || cfg->num_layers > NL || cfg->n_head != NH || cfg->n_pts != J)
         return DPK_E_UNSUPPORTED;
     int kind;
     if (cfg->coords_in == CIN && cfg->coords_out == COUT) kind = 0;
@@ -2569,6 +2649,12 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     dpk_handle* h = new dpk_handle();
     h->device = cfg->device;
     h->kind = kind;
+    h->num_layers = cfg->num_layers;
+    if (hipSetDevice(h->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return DPK_E_HIP;
+    }
     if (const char* pd = getenv("DPK_PHASE_DELAY")) h->phase_delay = atoi(pd);
     else h->phase_delay = WG_PER_CU == 2 ? 60000 : 0;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
@@ -2586,10 +2672,13 @@ void dpk_destroy(dpk_handle* h) {
     if (h->arena16) (void)hipFree(h->arena16);
     if (h->arenabf) (void)hipFree(h->arenabf);
     if (h->temb) (void)hipFree(h->temb);
-    if (h->coef) (void)hipFree(h->coef);
-    if (h->tproj) (void)hipFree(h->tproj);
-    if (h->tps) (void)hipFree(h->tps);
-    if (h->tps_ev) (void)hipEventDestroy(h->tps_ev);
+    if (h->tproj_zero) (void)hipFree(h->tproj_zero);
+    // hipFree waits for the device, so in-flight launches finish before their buffers go
+    if (h->sched) sched_free(h->sched);
+    for (Sched* s : h->retired) sched_free(s);
+    for (auto& b : h->eps_bufs)
+        if (b.p) (void)hipFree(b.p);
+    if (h->aux) (void)hipStreamDestroy(h->aux);
     for (auto* v : {&h->ev_used, &h->ev_free})
         for (auto& e : *v) {
             (void)hipEventDestroy(e.first);
@@ -2669,7 +2758,7 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
     const int cin = pose ? CIN_POSE : CIN, cout = pose ? COUT_POSE : COUT;
     float* A = h->h_arena.data();
     float w16max = 0.f;             // largest |64 w| of the split-fp16 GEMM weights
-    for (int l = 0; l < NL; ++l) {
+    for (int l = 0; l < h->num_layers; ++l) {
         float* Lw = A + (size_t)l * LAYER_FLOATS;
         const std::string at = "atten_layers." + std::to_string(l) + ".";
         const std::string gc = "gconv_layers." + std::to_string(l) + ".";
@@ -2796,13 +2885,13 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
     }
 #undef GET
     h->have_weights = true;
-    h->tps_valid = false;
     int rc = upload(h);
     if (rc || !pose) return rc;
     // the pose backbone adds no timestep projection: a zero row per layer (E_CHEB1 adds +0)
-    rc = ensure_tproj(h, 1);
-    if (rc) return rc;
-    HIPCHK(h, hipMemset(h->tproj, 0, (size_t)NL * D * 4));
+    if (!h->tproj_zero) {
+        HIPCHK(h, hipMalloc(&h->tproj_zero, (size_t)NL * D * 4));
+        HIPCHK(h, hipMemset(h->tproj_zero, 0, (size_t)NL * D * 4));
+    }
     return DPK_OK;
 }
 
@@ -2837,17 +2926,39 @@ int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* s
         c[s * 6 + 5] = (float)t;
     }
     HIPCHK(h, hipSetDevice(h->device));
-    if (h->coef && h->K < K) {
-        HIPCHK(h, hipFree(h->coef));
-        h->coef = nullptr;
+    sched_sweep(h);
+    // an identical schedule keeps its device buffers (and every graph captured with them)
+    if (h->sched && h->sched->K == K && h->sched->eta == eta && h->sched->h_coef == c) return DPK_OK;
+    Sched* s = new Sched();
+    const size_t tps_off = ((size_t)K * 6 + 3) / 4 * 4;
+    hipError_t e = hipMalloc(&s->buf, (tps_off + (size_t)K * NL * D) * 4);
+    if (e != hipSuccess) {
+        delete s;
+        return fail(h, DPK_E_HIP, std::string("dpk_set_schedule: hipMalloc: ") + hipGetErrorString(e) +
+                                      " (a schedule cannot be built while a graph is being captured)");
     }
-    if (!h->coef) HIPCHK(h, hipMalloc(&h->coef, (size_t)std::max(K, 1) * 6 * 4));
-    HIPCHK(h, hipMemcpy(h->coef, c.data(), c.size() * 4, hipMemcpyHostToDevice));
-    h->h_coef = c;
-    h->K = K;
-    h->eta = eta;
-    h->have_sched = true;
-    h->tps_valid = false;
+    s->coef = s->buf;
+    s->tps = s->buf + tps_off;
+    s->K = K;
+    s->eta = eta;
+    s->h_coef = c;
+    // a fresh buffer no launch has seen: the copy cannot race any stream
+    e = hipMemcpyAsync(s->coef, c.data(), c.size() * 4, hipMemcpyHostToDevice, h->aux);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->aux);
+    if (e != hipSuccess) {
+        sched_free(s);
+        return fail(h, DPK_E_HIP, std::string("dpk_set_schedule: coef upload: ") + hipGetErrorString(e));
+    }
+    if (h->have_weights) {
+        const int rc = sched_compute_tps(h, s);
+        if (rc) {
+            sched_free(s);
+            return rc;
+        }
+    }
+    if (h->sched) h->retired.push_back(h->sched);
+    h->sched = s;
+    sched_sweep(h);
     return DPK_OK;
 }
 
@@ -2871,25 +2982,48 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     if (rc) return rc;
     if (N == 0) return DPK_OK;
     HIPCHK(h, hipSetDevice(h->device));
-    rc = ensure_tproj(h, N);
-    if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(256), 0, st, h->temb, t, 1, h->tproj);
+    bool cap = false;
+    rc = capturing(h, st, &cap);
+    if (rc) return rc;
+    EpsBuf* buf = nullptr;
+    for (auto& b : h->eps_bufs)
+        if (b.st == st) buf = &b;
+    if (!buf) {
+        h->eps_bufs.push_back(EpsBuf{st, nullptr, 0});
+        buf = &h->eps_bufs.back();
+    }
+    if (buf->cap < N) {
+        if (cap)
+            return fail(h, DPK_E_STATE, "dpk_eps: this stream's projection buffer holds " + std::to_string(buf->cap) +
+                                            " poses; size it with an uncaptured call of >= N poses before capturing");
+        // earlier dpk_eps calls on this stream may still read the old buffer
+        HIPCHK(h, hipStreamSynchronize(st));
+        if (buf->p) HIPCHK(h, hipFree(buf->p));
+        buf->p = nullptr;
+        buf->cap = 0;
+        const int cap_new = std::max(N, 64);
+        HIPCHK(h, hipMalloc(&buf->p, (size_t)cap_new * NL * D * 4));
+        buf->cap = cap_new;
+    }
+    hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(256), 0, st, h->temb, t, 1, buf->p);
     HIPCHK(h, hipGetLastError());
     SampleArgs a{};
     a.arena = h->arena;
-    a.coef = h->coef;     // unused in eps mode
-    a.tproj = h->tproj;
+    a.coef = nullptr;     // unused in eps mode
+    a.tproj = buf->p;
     a.x_in = x;
     a.x_out = eps;
     a.N = N;
     a.K = 1;
     a.mask = h->mask;
+    a.num_layers = h->num_layers;
+    const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
+    if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     launch_sampler<M_EPS>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
-    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
+    if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
 }
 
@@ -2899,41 +3033,32 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     if (N < 0 || (N > 0 && (!x || !out))) return fail(h, DPK_E_INVALID, "dpk_sample: bad args");
     int rc = check_ready(h);
     if (rc) return rc;
-    if (!h->have_sched) return fail(h, DPK_E_STATE, "schedule not set");
+    Sched* sc = h->sched;
+    if (!sc) return fail(h, DPK_E_STATE, "schedule not set");
     if (N == 0) return DPK_OK;
+    if (sc->tps_gen != h->weights_gen) return fail(h, DPK_E_STATE, "dpk_sample: schedule projections are stale");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    if (!h->tps_valid) {
-        if (h->tps_cap < h->K) {
-            if (h->tps) HIPCHK(h, hipFree(h->tps));
-            h->tps = nullptr;
-            HIPCHK(h, hipMalloc(&h->tps, (size_t)h->K * NL * D * 4));
-            h->tps_cap = h->K;
-        }
-        if (!h->tps_ev) HIPCHK(h, hipEventCreateWithFlags(&h->tps_ev, hipEventDisableTiming));
-        hipLaunchKernelGGL(temb_kernel, dim3(h->K), dim3(256), 0, st, h->temb, h->coef + 5, 6, h->tps);
-        HIPCHK(h, hipGetLastError());
-        HIPCHK(h, hipEventRecord(h->tps_ev, st));
-        h->tps_stream = st;
-        h->tps_valid = true;
-    } else if (st != h->tps_stream && hipEventQuery(h->tps_ev) == hipErrorNotReady) {
-        HIPCHK(h, hipStreamWaitEvent(st, h->tps_ev, 0));
-    }
+    bool cap = false;
+    rc = capturing(h, st, &cap);
+    if (rc) return rc;
+    if (!cap) sched_sweep(h);
     if (xs) HIPCHK(h, hipMemcpyAsync(xs, x, (size_t)N * PE * 4, hipMemcpyDeviceToDevice, st));
     SampleArgs a{};
     a.arena = h->arena;
-    a.coef = h->coef;
-    a.tproj = h->tps;
+    a.coef = sc->coef;
+    a.tproj = sc->tps;
     a.x_in = x;
     a.x_out = out;
     a.xs = xs;
     a.x0s = x0s;
     a.N = N;
-    a.K = h->K;
+    a.K = sc->K;
     a.mask = h->mask;
-    a.eta = h->eta;
+    a.eta = sc->eta;
     a.seed = seed;
     a.phase_delay = h->phase_delay;
+    a.num_layers = h->num_layers;
 #if DPK_TRACE
     if (h->trace_step >= 0) {
         const size_t len = (size_t)((N + P - 1) / P) * NW * TRACE_SLOTS;
@@ -2947,12 +3072,13 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.trace = h->trace_step >= 0 ? h->trace : nullptr;
     a.trace_step = h->trace_step;
 #endif
+    const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
+    if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     launch_sampler<M_SAMPLE>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
-    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    return DPK_OK;
+    if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
+    return sched_note_use(h, sc, st, cap);
 }
 
 int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, int H, int root_mode,
@@ -2965,9 +3091,13 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     if (N == 0) return DPK_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
+    bool cap = false;
+    rc = capturing(h, st, &cap);
+    if (rc) return rc;
     SampleArgs a{};
     a.arena = h->arena;
-    a.tproj = h->tproj;   // zeros
+    a.num_layers = h->num_layers;
+    a.tproj = h->tproj_zero;   // zeros
     a.x_in = x2d;
     a.x_out = xyz;
     a.uvxyz = uvxyz;
@@ -2976,11 +3106,12 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     a.H = H;
     a.root_mode = root_mode;
     a.mask = h->mask;
+    const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
-    if (h->profiling && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
+    if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     launch_sampler<M_POSE>(h, dim3((N + P - 1) / P), st, a);
     HIPCHK(h, hipGetLastError());
-    if (h->profiling && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
+    if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;
 }
 
@@ -3019,15 +3150,20 @@ int dpk_ddim_update(dpk_handle* h, const float* xt, const float* et, float* xn, 
                     uint64_t seed, void* stream) {
     if (!h) return DPK_E_INVALID;
     if (n < 0 || (n > 0 && (!xt || !et || !xn))) return fail(h, DPK_E_INVALID, "dpk_ddim_update: bad args");
-    if (!h->have_sched) return fail(h, DPK_E_STATE, "schedule not set");
-    if (step < 0 || step >= h->K) return fail(h, DPK_E_INVALID, "dpk_ddim_update: step out of range");
+    Sched* sc = h->sched;
+    if (!sc) return fail(h, DPK_E_STATE, "schedule not set");
+    if (step < 0 || step >= sc->K) return fail(h, DPK_E_INVALID, "dpk_ddim_update: step out of range");
     if (n == 0) return DPK_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    bool cap = false;
+    int rc = capturing(h, st, &cap);
+    if (rc) return rc;
     const long long nb = (n + 255) / 256;
-    hipLaunchKernelGGL(ddim_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, xt, et, xn, x0, (long long)n,
-                       h->coef + step * 6, step, h->eta, (unsigned long long)seed);
+    hipLaunchKernelGGL(ddim_kernel, dim3((unsigned)nb), dim3(256), 0, st, xt, et, xn, x0, (long long)n,
+                       sc->coef + step * 6, step, sc->eta, (unsigned long long)seed);
     HIPCHK(h, hipGetLastError());
-    return DPK_OK;
+    return sched_note_use(h, sc, st, cap);
 }
 
 #if DPK_TRACE

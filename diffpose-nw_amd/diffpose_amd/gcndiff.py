@@ -71,6 +71,7 @@ class _HipModel:
         _lib.check(None, "dpk_create", rc)
         self._h = h
         self.n_pts = npts
+        self.num_layer = nl
         adj = adj.detach().cpu().numpy() if torch.is_tensor(adj) else np.asarray(adj)
         self.adj = np.ascontiguousarray(adj, dtype=np.float32)
         if self.adj.shape != (npts, npts):
@@ -84,7 +85,7 @@ class _HipModel:
     # -- nn.Module-like surface -------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True):
         """Accept the reference's states[0] (with/without 'module.'), torch tensors or numpy."""
-        sd = normalize_state_dict(state_dict, kind=self.KIND)
+        sd = normalize_state_dict(state_dict, kind=self.KIND, n_layers=self.num_layer)
         names = list(sd.keys())
         arrs = [np.ascontiguousarray(sd[k], dtype=np.float32) for k in names]
         c_names = (ctypes.c_char_p * len(names))(*[k.encode() for k in names])

@@ -147,14 +147,14 @@ def strip_module_prefix(sd) -> "OrderedDict[str, object]":
     return out
 
 
-def normalize_state_dict(sd, kind: str = "diff") -> "OrderedDict[str, np.ndarray]":
+def normalize_state_dict(sd, kind: str = "diff", n_layers: int = N_LAYERS) -> "OrderedDict[str, np.ndarray]":
     """Validate a GCNdiff (GCNpose) state_dict against the layout; return float32 numpy arrays.
 
     Raises KeyError for missing/unexpected keys and ValueError for shape
     mismatches, mirroring ``nn.Module.load_state_dict(strict=True)``.
     """
     sd = strip_module_prefix(sd)
-    shapes = param_shapes(kind=kind)
+    shapes = param_shapes(kind=kind, n_layers=n_layers)
     missing = [k for k in shapes if k not in sd]
     unexpected = [k for k in sd if k not in shapes]
     if missing or unexpected:
@@ -171,7 +171,7 @@ def normalize_state_dict(sd, kind: str = "diff") -> "OrderedDict[str, np.ndarray
     return out
 
 
-def load_checkpoint(path: str, kind: str = "diff") -> "OrderedDict[str, np.ndarray]":
+def load_checkpoint(path: str, kind: str = "diff", n_layers: int = N_LAYERS) -> "OrderedDict[str, np.ndarray]":
     """Load a reference checkpoint (list with states[0] = model state_dict) safely.
 
     Uses ``torch.load(weights_only=True)`` — never unpickles arbitrary objects.
@@ -181,4 +181,4 @@ def load_checkpoint(path: str, kind: str = "diff") -> "OrderedDict[str, np.ndarr
     states = torch.load(path, map_location="cpu", weights_only=True)
     if isinstance(states, (list, tuple)):
         states = states[0]
-    return normalize_state_dict(states, kind=kind)
+    return normalize_state_dict(states, kind=kind, n_layers=n_layers)

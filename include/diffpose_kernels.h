@@ -17,6 +17,18 @@
  *   - Poses are (N, 17, 5) uvxyz: N poses x 17 joints x 5 channels.
  *   - Return value 0 = OK, negative = error (DPK_E_*); dpk_last_error() has the text.
  *   - A handle is bound to one device and is not thread-safe: one handle per rank/thread.
+ *   - Stream order: launches (dpk_sample / dpk_eps / dpk_pose / dpk_ddim_update) may be in
+ *     flight on several streams at once.  dpk_set_schedule never rewrites a schedule a launch
+ *     may still read: it builds a new one, and the old one is freed only after every stream
+ *     that used it has passed its last launch.  dpk_eps keeps its per-pose timestep
+ *     projections in a buffer per caller stream.  dpk_load_weights / dpk_set_graph wait for
+ *     the device to drain before overwriting the weights (they are configuration calls).
+ *   - Graph capture (hipStreamBeginCapture / torch.cuda.graph): dpk_sample, dpk_eps, dpk_pose
+ *     and dpk_ddim_update may be captured.  A captured launch reads the schedule current at
+ *     capture time for the graph's whole life (a later dpk_set_schedule builds a new one and
+ *     leaves the captured one in place; it is freed by dpk_destroy); weights reloaded later
+ *     are seen by replays.  Nothing is allocated inside a captured call: dpk_eps needs one
+ *     uncaptured call of at least N poses on the stream first (else DPK_E_STATE).
  */
 #ifndef DIFFPOSE_KERNELS_H
 #define DIFFPOSE_KERNELS_H
@@ -38,8 +50,10 @@ typedef struct dpk_handle dpk_handle;
 
 /* Model hyper-parameters (configs/human36m_diffpose_uvxyz_*.yml model: section,
  * emd_dim = 4*hid_dim per models/gcndiff.py:68).  The kernels are compiled for
- * hid_dim 96, num_layer 5, n_head 4, n_pts 17 and coords_dim [5,5] (GCNdiff, the
- * denoiser) or [2,3] (GCNpose, the 2D->3D front-end; runners/diffpose_frame.py:138). */
+ * hid_dim 96, n_head 4, n_pts 17 and coords_dim [5,5] (GCNdiff, the denoiser) or [2,3]
+ * (GCNpose, the 2D->3D front-end; runners/diffpose_frame.py:138); num_layers (the
+ * config's num_layer, models/gcndiff.py:63-90) is a run-time value in 1..5 (the
+ * reference's configs all use 5).  Other values: DPK_E_UNSUPPORTED. */
 typedef struct {
     int hid_dim;
     int num_layers;
@@ -78,7 +92,10 @@ int dpk_set_mask(dpk_handle* h, const uint8_t* mask_host);
  * entries (compute_alpha, common/utils_diff.py:40-43); seq: K timesteps in
  * ascending order as built by test_hyber (runners/diffpose_frame.py:310-317);
  * eta as in common/utils_diff.py:61-63.  Step scalars are evaluated in fp32 in
- * the reference's operation order. */
+ * the reference's operation order.  Host-synchronous: builds a new device schedule
+ * (step scalars + per-step timestep projections, on a handle-internal stream) unless
+ * the schedule is unchanged; see "Stream order" above.  Not callable while a graph is
+ * being captured. */
 int dpk_set_schedule(dpk_handle* h, const float* alpha_bar, int n_alpha, const int* seq, int K, float eta);
 
 /* One denoiser evaluation eps = GCNdiff(x, mask, t) for N poses with a
@@ -86,7 +103,7 @@ int dpk_set_schedule(dpk_handle* h, const float* alpha_bar, int n_alpha, const i
 int dpk_eps(dpk_handle* h, const float* x_dev, const float* t_dev, float* eps_dev, int N, void* stream);
 
 /* The whole K-step reverse loop of generalized_steps for N poses in ONE
- * persistent kernel (plus one timestep-embedding kernel).
+ * persistent kernel (the per-step timestep projections come with the schedule).
  *   x_dev   [N,17,5] input x (= xs[0])
  *   out_dev [N,17,5] final sample xs[-1]
  *   xs_dev  [K+1,N,17,5] or NULL: full trajectory xs (xs[0] copied from x_dev)
