@@ -66,183 +66,9 @@ __device__ __forceinline__ void tr_stamp() {
 #define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
 #endif
 
-namespace dpk {
 
-// ---------------------------------------------------------------------------------------
-// compile-time model shape (configs/human36m_diffpose_uvxyz_cpn.yml:9-16)
-constexpr int J = 17;        // joints (n_pts)
-constexpr int D = 96;        // hid_dim
-constexpr int D2 = 192;      // GraphNet hidden (2*hid)
-constexpr int D3 = 288;      // QKV / Chebyshev-stacked width
-constexpr int E = 384;       // emd_dim = 4*hid
-constexpr int NL = 5;        // num_layer
-constexpr int NH = 4;        // n_head
-constexpr int DK = 24;       // d_k
-constexpr int CIN = 5;       // coords_dim[0]
-constexpr int COUT = 5;      // coords_dim[1]
-constexpr int PE = J * CIN;  // floats per pose (85)
-
-// workgroup tile
-#ifndef DPK_ATTN_MMA
-#define DPK_ATTN_MMA 1       // attention on the matrix cores (attention_mma) or on DPP rows (attention)
-#endif
-#ifndef DPK_LN_FUSE
-#define DPK_LN_FUSE 0        // 1: fp32 mode: LayerNorm statistics from the producing GEMM epilogue, applied in the consumer
-#endif
-#ifndef DPK_LN1_FUSE
-#define DPK_LN1_FUSE 0       // 1: as DPK_LN_FUSE for LN1 only (O-proj epilogue statistics, applied by graph1)
-#endif
-#ifndef DPK_P
-#define DPK_P 4              // poses per workgroup: 4 (one workgroup per CU) or 2 (two per CU)
-#endif
-constexpr int P = DPK_P;     // poses per workgroup
-constexpr int R = P * J;     // 68 (34) rows
-static_assert(P == 4 || P == 2, "4 or 2 poses per workgroup");
-// P = 2 (two workgroups per CU, 34-row GEMMs) was measured slower at v5 (62.4k vs 74k poses/s)
-// and at v9 (72.8k vs 82.6k); the phases added since (MFMA attention, GraphNet MFMA, split-GEMM
-// modes) are written for P = 4, so the option is closed.
-static_assert(P == 4, "DPK_P=2 is no longer maintained (see DESIGN.md section 6)");
-constexpr int WG_PER_CU = P == 4 ? 1 : 2;
-constexpr int NT = 256;      // threads (4 waves, one per SIMD)
-constexpr int NW = NT / 64;
-constexpr int LDX = 104;     // LDS row stride, 96-wide buffers  (≡40 mod 64: conflict-free b128 A reads)
-constexpr int LD2 = 296;     // LDS row stride, 288-wide buffer  (≡40 mod 64)
-
-// LDS carve (floats)
-constexpr int SM_XS = 0;                    // residual stream   [R][LDX]
-constexpr int SM_B1 = SM_XS + R * LDX;      // 96-wide scratch   [R][LDX]
-constexpr int SM_B2 = SM_B1 + R * LDX;      // 288-wide scratch  [R][LD2]
-constexpr int SM_XST = SM_B2 + R * LD2;     // pose state x_t    [R][5]
-constexpr int SM_LNP = SM_XST + ((R * CIN + 3) / 4) * 4;   // LayerNorm gains/shifts of all layers [NL][4][D]
-constexpr int SM_ST = SM_LNP + NL * 4 * D;                  // LayerNorm row statistics (fused LN, below)
-constexpr int ST_TAIL = 64 * 4;                             // [64 main rows][mean0, M2_0, mean1, M2_1]
-constexpr int SM_TC = SM_ST + ST_TAIL + 4 * 4 * 4;          // + [4 tail rows][4 waves][n, mean, M2, -]
-constexpr int SM_FLOATS = SM_TC + 2 * J * J;                // dense T1, T2 for the output ChebConv
-static_assert(SM_FLOATS * 4 <= 160 * 1024, "LDS budget");
-
-// packed-weight blocks: one block = 16 cols x 16 k = 64 lanes x float4
-constexpr int BLK = 256;
-constexpr int KB_D = D / 16, KB_D2 = D2 / 16, KB_D3 = D3 / 16;   // 6, 12, 18
-// per-layer offsets (floats) in the weight arena
-constexpr int OFF_QKV = 0;                                  // [18 ct][6 kb]
-constexpr int OFF_O = OFF_QKV + 18 * KB_D * BLK;            // [6][6]
-constexpr int OFF_FC1 = OFF_O + 6 * KB_D * BLK;             // [12][6]
-constexpr int OFF_FC2 = OFF_FC1 + 12 * KB_D * BLK;          // [6][12]
-constexpr int OFF_C1 = OFF_FC2 + 6 * KB_D2 * BLK;           // [6][18]
-constexpr int OFF_C2 = OFF_C1 + 6 * KB_D3 * BLK;            // [6][18]
-constexpr int OFF_BQKV = OFF_C2 + 6 * KB_D3 * BLK;
-constexpr int OFF_BO = OFF_BQKV + D3;
-constexpr int OFF_BFC1 = OFF_BO + D;
-constexpr int OFF_BFC2 = OFF_BFC1 + D2;
-constexpr int OFF_BC1 = OFF_BFC2 + D;
-constexpr int OFF_BC2 = OFF_BC1 + D;
-constexpr int OFF_LN0A = OFF_BC2 + D;
-constexpr int OFF_LN0B = OFF_LN0A + D;
-constexpr int OFF_LN1A = OFF_LN0B + D;
-constexpr int OFF_LN1B = OFF_LN1A + D;
-constexpr int OFF_LG = OFF_LN1B + D;                        // 17x17
-constexpr int OFF_LGF = ((OFF_LG + J * J + 63) / 64) * 64;  // graph_mma operands: [5 k][64 lanes] L^T, then row 16
-constexpr int LAYER_FLOATS = OFF_LGF + 2 * 5 * 64;
-constexpr int OFF_WIN = NL * LAYER_FLOATS;                  // [6 ct][1 kb]  (K=15 padded to 16)
-constexpr int OFF_WOUT = OFF_WIN + 6 * 1 * BLK;             // [1 ct][18 kb] (N=5 padded to 16)
-constexpr int OFF_BIN = OFF_WOUT + 1 * KB_D3 * BLK;
-constexpr int OFF_BOUT = OFF_BIN + D;                       // 16 (5 used)
-constexpr int OFF_CHEB = OFF_BOUT + 16;                     // dense T1 [17x17] then T2 [17x17]
-constexpr int OFF_CHEBS = OFF_CHEB + 2 * J * J;             // H36M-sparse T1 (49) then T2 (87) values
-constexpr int ARENA_FLOATS = ((OFF_CHEBS + 136 + 63) / 64) * 64;
-
-// Split-fp16 GEMM arena (gemm mode 1): per layer, each GEMM's weights x W16_SCALE split into
-// fp16 hi + lo parts, packed as 16x16x32 B fragments: block (16 cols x 32 k) = [hi 1 KiB | lo 1 KiB],
-// lane l holding W[k = kb*32 + 8*(l>>4) + i][n = ct*16 + (l&15)] in half i = 0..7.  Byte offsets.
-constexpr float W16_SCALE = 64.0f;            // keeps the lo parts of O(0.01) weights in fp16's normal range
-constexpr int BLK16 = 2048;
-constexpr int KB32_D = D / 32, KB32_D2 = D2 / 32, KB32_D3 = D3 / 32;   // 3, 6, 9
-constexpr int O16_QKV = 0;                                             // [18 ct][3 kb]
-constexpr int O16_O = O16_QKV + 18 * KB32_D * BLK16;                   // [6][3]
-constexpr int O16_FC1 = O16_O + 6 * KB32_D * BLK16;                    // [12][3]
-constexpr int O16_FC2 = O16_FC1 + 12 * KB32_D * BLK16;                 // [6][6]
-constexpr int O16_C1 = O16_FC2 + 6 * KB32_D2 * BLK16;                  // [6][9]
-constexpr int O16_C2 = O16_C1 + 6 * KB32_D3 * BLK16;                   // [6][9]
-constexpr int LAYER16_BYTES = O16_C2 + 6 * KB32_D3 * BLK16;
-constexpr int ARENA16_BYTES = NL * LAYER16_BYTES;
-
-// timestep-MLP arena (transposed nn.Linear weights: [in][out])
-constexpr int TOFF_W0 = 0;                    // [96][384]
-constexpr int TOFF_B0 = TOFF_W0 + D * E;
-constexpr int TOFF_W1 = TOFF_B0 + E;          // [384][384]
-constexpr int TOFF_B1 = TOFF_W1 + E * E;
-constexpr int TOFF_WP = TOFF_B1 + E;          // [5][384][96]
-constexpr int TOFF_BP = TOFF_WP + NL * E * D; // [5][96]
-constexpr int TEMB_FLOATS = TOFF_BP + NL * D;
-
-constexpr float SQRT_DK = 4.898979485566356f;   // float(math.sqrt(24)), divisor
-constexpr float LN_EPS = 1e-6f;                         // LayerNorm eps (GraFormer.py:60)
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// packed fp32 fma (v_pk_fma_f32: two lanes of work per instruction)
-__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f32x2 splat2(float x) { return f32x2{x, x}; }
-
-// ---- split-fp16 activation layout (gemm mode 1) -------------------------------------------
-// A GEMM input row of K fp32 values is stored as K/8 chunks of 32 bytes: [hi(8 x fp16) | lo(8 x fp16)]
-// with hi = fp16(v), lo = fp16(v - hi).  A lane's 16x16x32 A fragment (8 consecutive k) is then
-// two 16-byte LDS reads, with no conversion in the k-loop.  Same bytes per row as fp32.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-// SP = 1: hi/lo fp16 pair (gemm mode 1, split-fp16); SP = 2: hi/lo bf16 pair (gemm mode 2,
-// bf16 GEMMs, which read only the hi half).  Both keep the same 32-byte chunk layout.
-template <int SP>
-__device__ __forceinline__ void split_pair(f32x2 v, f16x2& hi, f16x2& lo) {
-    if constexpr (SP == 2) {
-        const bf16x2 h = __builtin_convertvector(v, bf16x2);
-        const bf16x2 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), bf16x2);
-        hi = __builtin_bit_cast(f16x2, h);
-        lo = __builtin_bit_cast(f16x2, l);
-    } else {
-        hi = __builtin_convertvector(v, f16x2);
-        lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x2), f16x2);
-    }
-}
-// 4 consecutive columns col..col+3 (col % 4 == 0) of a split row
-template <int SP>
-__device__ __forceinline__ void split_store4(char* row, int col, f32x4 v) {
-    f16x2 h0, l0, h1, l1;
-    split_pair<SP>(f32x2{v[0], v[1]}, h0, l0);
-    split_pair<SP>(f32x2{v[2], v[3]}, h1, l1);
-    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
-    *reinterpret_cast<f16x4*>(p) = f16x4{h0[0], h0[1], h1[0], h1[1]};
-    *reinterpret_cast<f16x4*>(p + 16) = f16x4{l0[0], l0[1], l1[0], l1[1]};
-}
-template <int SP>
-__device__ __forceinline__ void split_store2(char* row, int col, f32x2 v) {   // col % 2 == 0
-    f16x2 h, l;
-    split_pair<SP>(v, h, l);
-    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
-    *reinterpret_cast<f16x2*>(p) = h;
-    *reinterpret_cast<f16x2*>(p + 16) = l;
-}
-template <int SP>
-__device__ __forceinline__ void split_store1(char* row, int col, float v) {
-    f16x2 h, l;
-    split_pair<SP>(f32x2{v, 0.f}, h, l);
-    char* p = row + (col >> 3) * 32 + (col & 7) * 2;
-    *reinterpret_cast<_Float16*>(p) = h[0];
-    *reinterpret_cast<_Float16*>(p + 16) = l[0];
-}
-
-// Kernel modes: the K-step sampler (GCNdiff + DDIM), one GCNdiff eps evaluation, or one
-// GCNpose forward (models/gcnpose.py:101-113: the same backbone without the timestep
-// embedding, coords 2 -> 3), which also builds the sampler's uvxyz input
-// (runners/diffpose_frame.py:337-342).
-enum { M_SAMPLE = 0, M_EPS = 1, M_POSE = 2 };
-constexpr int CIN_POSE = 2, COUT_POSE = 3;
-
+// Launch arguments of the sampler kernel, shared by both tile sizes (dpk_sampler.inc).
+namespace dpk_shared {
 struct SampleArgs {
     const float* arena;   // packed weights
     const float* coef;    // [K][6] = sqrt(1-at), sqrt(at), sqrt(an), c1, c2, t
@@ -259,2031 +85,27 @@ struct SampleArgs {
     unsigned mask;        // 17-bit key mask
     float eta;
     unsigned long long seed;
-    int phase_delay;      // two workgroups per CU: start delay (cycles) of the grid's second half
+    int pose_off;         // first pose of this launch (a batch split over two launches, see launch_sampler)
     int num_layers;       // GraAttenLayer + _ResChebGC_diff pairs run (config num_layer, 1..NL)
 #if DPK_TRACE
     unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
     int trace_step;
 #endif
 };
-constexpr int TRACE_SLOTS = 256;
+}  // namespace dpk_shared
 
-// ---------------------------------------------------------------------------------------
-// counter-based normal noise for eta > 0 (Philox4x32-10 + Box-Muller)
-__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        c[1] = (uint32_t)p1;
-        c[3] = (uint32_t)p0;
-        c[0] = n0;
-        c[2] = n2;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
+#define DPK_P 4
+namespace dpk {
+#include "dpk_sampler.inc"
+}  // namespace dpk
+#undef DPK_P
+#define DPK_P 2
+namespace dpk2 {
+#include "dpk_sampler.inc"
+}  // namespace dpk2
+#undef DPK_P
 
-__device__ __forceinline__ float normal_noise(unsigned long long seed, int step, long long idx) {
-    uint32_t c[4] = {(uint32_t)idx, (uint32_t)((unsigned long long)idx >> 32), (uint32_t)step, 0x5EEDu};
-    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
-    const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);            // [0, 1)
-    return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
-}
-
-// DDIM update for one element (common/utils_diff.py:59-65), fp32, no contraction:
-// x0 = (xt - et*sqrt(1-at)) / sqrt(at);  x' = sqrt(an)*x0 + c1*z + c2*et
-__device__ __forceinline__ void ddim_elem(const float* cf, float xt, float et, float z, float& x0, float& xn) {
-    x0 = (xt - et * cf[0]) / cf[1];
-    xn = (cf[2] * x0 + cf[3] * z) + cf[4] * et;
-}
-
-// DPP row (16-lane) rotations and all-reduces
-template <int J>
-__device__ __forceinline__ float row_ror(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x),
-                                                                 0x120 + J, 0xf, 0xf, false));
-}
-
-// Sum over the 4 lane rows (l, l^16, l^32, l^48), result in every lane, on the VALU: a
-// v_permlane32_swap / v_permlane16_swap of two copies of v leaves (v, partner) split across
-// the two registers, so their sum is v + partner in every lane (tools/permlane_probe.hip; the
-// clang builtins return a mis-assigned pair on this toolchain, hence the inline asm).  Replaces
-// two LDS-crossbar shuffles.
-__device__ __forceinline__ float sum4rows(float v) {
-    float a = v, b = v;
-    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    const float s1 = a + b;
-    float c = s1, d = s1;
-    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
-    return c + d;
-}
-
-// Reduce-scatter of 4 registers over the 4 lane rows: lane l returns the sum over rows of
-// register (l>>4) at row position l&15, summed ((row0 + row2) + (row1 + row3)) like sum4rows.
-// 3 permlane swaps for 4 values instead of sum4rows' 8 (tools/rs4_probe.hip checks the map).
-__device__ __forceinline__ float rs4rows(float v0, float v1, float v2, float v3) {
-    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v0), "+v"(v2));
-    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v1), "+v"(v3));
-    float a = v0 + v2, b = v1 + v3;
-    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    return a + b;
-}
-
-// Launder a value through an empty asm so LLVM cannot hoist per-thread address math out
-// of the K-step / layer loops of the persistent kernel (hoisted, it stays live across
-// every phase and spills).
-__device__ __forceinline__ int opaque(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-// ---------------------------------------------------------------------------------------
-// GEMM over the workgroup's 68 rows.  Rows 0..63 are 4 MFMA row tiles (v_mfma_f32_16x16x4_f32);
-// the 4 leftover rows 64..67 ("tail") run on v_mfma_f32_4x4x1_16b_f32 inside the same k-loop,
-// fed by the B fragments already in registers (TM_MFMA4 below; in a QKV-shaped k-block the 20
-// tail MFMAs cost 8.8 cycles each beside the 72 16x16x4 ones, tools/mfma_mix_probe.hip; VALU
-// FMAs for these rows (v4) cost ~10 cycles each, a padded 16-row tile 25 % of the GEMM).
-//
-// MFMA operand maps: lane l holds A[row rt*16+(l&15)][k = kb*16 + 4*(l>>4) + j] for sub-step j,
-// and the packed B block holds W[k = same][n = ct*16 + (l&15)] (a consistent permutation of k).
-// Tail: the 4x4x1 accumulators hold partial sums per k-slice (lane group), reduce-scattered by
-// permlane swaps in the epilogue (rs4rows).
-//
-// B blocks are fetched with buffer loads: one VGPR offset (lane*16) shared by every load and the
-// block offset in SGPR soffset, so the k-loop does no VALU address arithmetic.  A comes from one
-// LDS buffer per GEMM (the Chebyshev GEMMs read [T1X | T2X | X] from B2, see cheb_prep), which
-// keeps the loop body a single basic block: loads are unconditional (last pair peeled) and the
-// compiler emits exact vmcnt/lgkmcnt waits instead of draining at a join.
-struct BSrc {
-    __amdgpu_buffer_rsrc_t rsrc;
-    int voff;      // lane * 16
-    int sbase;     // byte offset of this wave's first column tile (wave-uniform)
-    __device__ __forceinline__ f32x4 load(int blk) const {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, sbase + blk * 1024, 0));
-    }
-};
-
-// Packed B-fragment blocks of a GEMM with NC column tiles and KB k-blocks: [NC][KB][64 lanes][4].
-template <int NC, int KB>
-__device__ __forceinline__ BSrc bsrc(const float* Bp, int ct0, int lane) {
-    BSrc s;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, NC * KB * 1024, 0x00020000);
-    s.voff = lane * 16;
-    s.sbase = ct0 * KB * 1024;
-    return s;
-}
-
-// Tail modes: TM_VALU — TR tail rows per wave on the VALU (scalar fma per MFMA);
-// TM_MFMA4 — all 4 tail rows on v_mfma_f32_4x4x1_16b_f32 for NQ = ceil(NCW/2) of the wave's
-// column tiles.  The 4x4x1 form reads the SAME B fragment as the 16x16x4 MFMAs (block b = l>>2
-// holds W[k = kb*16 + 4*(l>>4) + j][col 4*(b&3) + (l&3)]), and its A operand is one float per
-// lane: tail row l&3 at the lane group's k.  D reg r of lane l = partial sum (tail row r,
-// column l&15, k-slice l>>4).  The two waves of a column half split the tail column tiles: the
-// second wave processes its tiles rotated by NQ (rotation lives in SGPR load offsets and store
-// addresses only), so the tail tiles are local indices 0..NQ-1 for both.
-enum { TM_NONE = 0, TM_VALU = 1, TM_MFMA4 = 2 };
-
-// TRANS: the MFMA computes the transposed tile (operands swapped: the packed weight fragment
-// is the A operand, the activation fragment the B operand; both registers are unchanged), so
-// lane l ends up with 4 consecutive COLUMNS 4*(l>>4)..+3 of row l&15 and the epilogue moves
-// one 16-byte vector per tile (ds_write_b128 / ds_read_b128) instead of four 4-byte ones.
-template <int NR, int NCW, int TM, int TR, int KB, bool TRANS = true>
-struct GemmTile {
-    static constexpr int TA = TM == TM_VALU ? TR : 1;    // tail A fragments per ring slot
-    static constexpr int NQ = TM == TM_MFMA4 ? (NCW + 1) / 2 : 1;
-    f32x4 acc[NR][NCW];
-    float tl[NCW][TA];      // TM_VALU: tail partial sums over this lane's k's
-    f32x4 tacc[NQ];         // TM_MFMA4: 4x4x1 accumulators
-    int aoff[NR], toff[TA];
-
-    __device__ __forceinline__ void loadA(f32x4 (&a)[NR], f32x4 (&t)[TA], const float* A, int kb) const {
-#pragma unroll
-        for (int i = 0; i < NR; ++i) a[i] = *reinterpret_cast<const f32x4*>(A + aoff[i] + kb * 16);
-        if constexpr (TM != TM_NONE) {
-#pragma unroll
-            for (int i = 0; i < TA; ++i) t[i] = *reinterpret_cast<const f32x4*>(A + toff[i] + kb * 16);
-        }
-    }
-    __device__ __forceinline__ static void loadB(f32x4 (&b)[NCW], const BSrc& s, const int (&soff)[NCW], int kb) {
-#pragma unroll
-        for (int c = 0; c < NCW; ++c)
-            b[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c] + kb * 1024, 0));
-    }
-    // FIRST: the GEMM's first k-step takes C = 0 as an inline constant (no accumulator zeroing:
-    // ~100 v_accvgpr_write per wave and GEMM otherwise)
-    template <bool FIRST = false>
-    __device__ __forceinline__ void mma(const f32x4 (&a)[NR], const f32x4 (&t)[TA], const f32x4 (&b)[NCW]) {
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-#pragma unroll
-                for (int c = 0; c < NCW; ++c) {
-                    const f32x4 cin = (FIRST && j == 0) ? z : acc[i][c];
-                    acc[i][c] = TRANS ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[c][j], a[i][j], cin, 0, 0, 0)
-                                      : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][j], b[c][j], cin, 0, 0, 0);
-                }
-            if constexpr (TM == TM_VALU) {
-#pragma unroll
-                for (int c = 0; c < NCW; ++c)
-#pragma unroll
-                    for (int r = 0; r < TR; ++r) tl[c][r] = fmaf(t[r][j], b[c][j], tl[c][r]);
-            } else if constexpr (TM == TM_MFMA4) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    tacc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(b[q][j], t[0][j], (FIRST && j == 0) ? z : tacc[q], 0, 0, 0);
-            }
-        }
-    }
-    // keep the ring's program order: this half's MFMAs, then its slot's loads; nothing crosses
-    // (otherwise the scheduler sinks the loads next to their consumers)
-    __device__ __forceinline__ static void schedule_half() { __builtin_amdgcn_sched_barrier(0); }
-};
-
-// B fragments of a GEMM's first two k-blocks, loaded before the phase that precedes the GEMM
-// (weights do not depend on activations) so the L2 latency hides under that phase.
-template <int NCW>
-struct BPre {
-    f32x4 b0[NCW], b1[NCW];
-};
-
-// Wave roles in the workgroup GEMM: column half ch(w) and index within the pair of waves that
-// share it, pr(w).  68 rows: wave w = row tiles 2*(w>>1)+{0,1} of column half w&1; 34 rows:
-// row tile w&1 of column half w>>1.
-__device__ __forceinline__ int gemm_ch(int wave) { return R == 68 ? (wave & 1) : (wave >> 1); }
-__device__ __forceinline__ int gemm_pr(int wave) { return R == 68 ? (wave >> 1) : (wave & 1); }
-
-// Column rotation of wave `wave` within its column half (TM_MFMA4 tail split, see GemmTile).
-template <int NCW>
-__device__ __forceinline__ int col_rot(int wave) { return gemm_pr(wave) ? (NCW + 1) / 2 : 0; }
-
-// SGPR byte offsets of the wave's NCW column tiles' first k-block, rotation applied.
-template <int NCW, int KB>
-__device__ __forceinline__ void tile_offsets(int (&soff)[NCW], int sbase, int rot) {
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) {
-        const int cc = c + rot;
-        soff[c] = sbase + (cc >= NCW ? cc - NCW : cc) * KB * 1024;
-    }
-}
-
-template <int NC, int KB>
-__device__ __forceinline__ BPre<NC / 2> gemm_prefetch(const float* Bp, int wave, int lane) {
-    constexpr int NCW = NC / 2;
-    const BSrc s = bsrc<NC, KB>(Bp, gemm_ch(wave) * NCW, lane);
-    int soff[NCW];
-    tile_offsets<NCW, KB>(soff, s.sbase, col_rot<NCW>(wave));
-    BPre<NCW> pre;
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) {
-        pre.b0[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c], 0));
-        pre.b1[c] = KB > 1 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, s.voff, soff[c] + 1024, 0))
-                           : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    return pre;
-}
-
-// Epilogue modes (out = acc + bias[col]):
-//   E_STORE       dst = out                       (QKV, gconv_input)
-//   E_STORE_RELU  dst = relu(out)                 (GraphNet fc1)
-//   E_RESID       dst = dst + out                 (attention O-proj)
-//   E_RESID_RELU  dst = dst + relu(out)           (Cheb2 of _ResChebGC_diff)
-//   E_CHEB1       dst = relu(out) + tproj[col]    (Cheb1 + temb_proj injection)
-//   E_STORE_NB    dst = acc (no bias)             (GraphNet fc2 before its graph product)
-// Bias / temb columns are loaded into registers before the k-loop and residual values are
-// read in one batch, so the epilogue is LDS + VALU only (no per-element global round trip).
-enum { E_STORE = 0, E_STORE_RELU, E_RESID, E_RESID_RELU, E_CHEB1, E_STORE_NB };
-
-struct EpiArgs {
-    float* dst;
-    int ldd;
-    const float* bias;
-    const float* tproj;     // E_CHEB1: temb_proj row (sample mode) or per-pose base (eps mode)
-    int tproj_pose_stride;  // 0: one row for all poses; else floats between consecutive poses
-    int pose0;              // global index of the workgroup's first pose (eps mode clamp)
-    int pose_max;           // N-1
-    float* st = nullptr;    // STATS epilogues: LayerNorm partial statistics of the rows written (LDS)
-};
-
-// ---- fused LayerNorm (fp32 GEMM mode, DPK_LN_FUSE) ------------------------------------------
-// GraFormer's LayerNorm (GraFormer.py:58-70) is split across the phases around it: the GEMM
-// epilogue that writes the residual stream x (gconv_input, O-proj, Cheb2) also reduces, per
-// row and per 48-column half it owns, (mean, M2 = sum (x - mean)^2) over its final values (rows
-// 64..67: per wave, (n, mean, M2) over the tail columns it owns), into LDS; the consumer (the QKV
-// GEMM's A-operand ring for LN0, the GraphNet product for LN1) merges the partials with Chan et
-// al.'s pairwise update and applies a*(x-mean)/(std+eps)+b to its operand registers, so the LN
-// phase, its LDS round trip and its barrier disappear.  std is the unbiased (/95) one.
-// merge partial b into a: f = n_b / (n_a + n_b), g = n_a n_b / (n_a + n_b)
-__device__ __forceinline__ void chan_merge(float& m, float& M2, float mb, float M2b, float f, float g) {
-    const float d = mb - m;
-    m = fmaf(d, f, m);
-    M2 = (M2 + M2b) + (d * d) * g;
-}
-// 1/d to ~0.5 ulp: v_rcp_f32 plus one Newton step
-__device__ __forceinline__ float rcp_nr(float d) {
-    const float r = __builtin_amdgcn_rcpf(d);
-    return fmaf(r, fmaf(-d, r, 1.0f), r);
-}
-// (mean, 1/(std + eps)) of workgroup row `row` from the partials in st
-template <int RR = R>   // instantiated only by fused-LN kernels (R == 68)
-__device__ __forceinline__ f32x2 ln_row_norm(const float* st, int row) {
-    constexpr int RM = RR - RR % 16;
-    float m, M2;
-    if (row < RM) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(st + row * 4);
-        const float d = v[2] - v[0];
-        m = (v[0] + v[2]) * 0.5f;
-        M2 = (v[1] + v[3]) + (d * d) * 24.0f;            // n_a n_b / (n_a + n_b) = 48*48/96
-    } else {
-        // tail columns per wave (gemm_wave, N = 96): waves 0,1 own 32, waves 2,3 own 16
-        static_assert(RR == 68, "tail partial counts");
-        const float* t = st + ST_TAIL + (row - RM) * 16;
-        const f32x4 p0 = *reinterpret_cast<const f32x4*>(t), p1 = *reinterpret_cast<const f32x4*>(t + 4);
-        const f32x4 p2 = *reinterpret_cast<const f32x4*>(t + 8), p3 = *reinterpret_cast<const f32x4*>(t + 12);
-        m = p0[1];
-        M2 = p0[2];
-        chan_merge(m, M2, p1[1], p1[2], 0.5f, 16.0f);                    // 32 + 32
-        chan_merge(m, M2, p2[1], p2[2], 0.2f, 12.8f);                    // 64 + 16
-        chan_merge(m, M2, p3[1], p3[2], 1.0f / 6.0f, 80.0f / 6.0f);      // 80 + 16
-    }
-    constexpr float RD1 = 1.0f / (float)(D - 1);
-    const float den = __builtin_amdgcn_sqrtf(M2 * RD1) + LN_EPS;   // v_sqrt_f32 (1 ulp)
-    return f32x2{m, rcp_nr(den)};
-}
-// a*(x-mean)/(std+eps)+b on 4 consecutive columns of one row
-__device__ __forceinline__ f32x4 ln_apply4(f32x4 x, f32x2 nrm, f32x4 gain, f32x4 shift) {
-    return __builtin_elementwise_fma((x - nrm[0]) * nrm[1], gain, shift);
-}
-
-template <int MODE>
-__device__ __forceinline__ float epi_value(float acc, float bias, float tp, float old) {
-    const float v = acc + bias;
-    if constexpr (MODE == E_STORE_NB) return acc;
-    else if constexpr (MODE == E_STORE) return v;
-    else if constexpr (MODE == E_STORE_RELU) return fmaxf(v, 0.f);
-    else if constexpr (MODE == E_RESID) return old + v;
-    else if constexpr (MODE == E_RESID_RELU) return old + fmaxf(v, 0.f);
-    else return fmaxf(v, 0.f) + tp;
-}
-
-// the same on 4 columns as packed-f32 vector ops (v_pk_add_f32); identical roundings
-template <int MODE>
-__device__ __forceinline__ f32x4 epi_value4(f32x4 acc, f32x4 bias, f32x4 tp, f32x4 old) {
-    if constexpr (MODE == E_STORE_NB) return acc;
-    const f32x4 v = acc + bias;
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (MODE == E_STORE) return v;
-    else if constexpr (MODE == E_STORE_RELU) return __builtin_elementwise_max(v, z);
-    else if constexpr (MODE == E_RESID) return old + v;
-    else if constexpr (MODE == E_RESID_RELU) return old + __builtin_elementwise_max(v, z);
-    else return __builtin_elementwise_max(v, z) + tp;
-}
-
-__device__ __forceinline__ float tproj_at(const EpiArgs& e, int row, int col, float tcol) {
-    if (e.tproj_pose_stride == 0) return tcol;
-    const int pose = min(e.pose0 + row / J, e.pose_max);
-    return e.tproj[(size_t)pose * e.tproj_pose_stride + col];
-}
-
-
-// One wave: row tiles [rt0, rt0+NR) on MFMA plus the tail (TM) over NCW column tiles from ct0,
-// visited in rotated order (local tile c = global ct0 + (c + rot) mod NCW); 2-stage register
-// ring (named buffers, loop unrolled by 2, last pair peeled).
-// STATS: the epilogue also writes the fused-LayerNorm partials of its rows (N = 96 only);
-// LNA: the A operand is raw x, normalised in registers with the statistics in `lst` and the
-// gains/shifts lg/lb (LDS) before it feeds the MFMAs (fused LayerNorm, see ln_row_norm).
-// XS2: k-blocks 0 .. 2S-1 of A come from AX (row stride ldx) instead of A: the Chebyshev GEMMs'
-// T0 = x block is read where x lives (cheb_prep XSKIP).  Those k-blocks are loaded only by the
-// prologue and the peeled first ring pass, so the choice is compile-time.
-template <int NR, int NCW, int TM, int TR, int NC, int KB, int MODE, bool STATS = false, bool LNA = false,
-          bool XS2 = false>
-__device__ __forceinline__ void gemm_wave(const float* A, int lda, const float* Bp, int rt0, int ct0, int rot,
-                                          int trow0, bool tail_dup, int lane, const EpiArgs& e,
-                                          const BPre<NCW>& pre, const float* lst = nullptr,
-                                          const float* lg = nullptr, const float* lb = nullptr,
-                                          const float* AX = nullptr, int ldx = 0) {
-    using T = GemmTile<NR, NCW, TM, TR, KB>;
-    constexpr int TA = T::TA, NQ = T::NQ;
-    static_assert(KB == 1 || KB % 2 == 0, "k-blocks in pairs");
-    lane = opaque(lane);
-    T g;   // accumulators: set by the first k-step (mma<true>)
-#pragma unroll
-    for (int c = 0; c < NCW; ++c)
-#pragma unroll
-        for (int r = 0; r < TA; ++r) g.tl[c][r] = 0.f;
-    const int rl = lane & 15, kq = (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) g.aoff[i] = ((rt0 + i) * 16 + rl) * lda + kq;
-    if constexpr (TM == TM_MFMA4) {
-        g.toff[0] = (trow0 + (lane & 3)) * lda + kq;
-    } else {
-#pragma unroll
-        for (int i = 0; i < TA; ++i) g.toff[i] = (trow0 + i) * lda + kq;
-    }
-    int xoff[NR], xtoff = 0;
-    if constexpr (XS2) {
-        static_assert(TM == TM_MFMA4, "XS2: 4x4x1 tail rows");
-#pragma unroll
-        for (int i = 0; i < NR; ++i) xoff[i] = ((rt0 + i) * 16 + rl) * ldx + kq;
-        xtoff = (trow0 + (lane & 3)) * ldx + kq;
-    }
-    int gcol[NCW];                                  // global column tile of local tile c (uniform)
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) {
-        const int cc = c + rot;
-        gcol[c] = ct0 + (cc >= NCW ? cc - NCW : cc);
-    }
-    // bias (and sample-mode temb projection) of this lane's 4 output columns per tile
-    f32x4 bias4[NCW], tp4[NCW];
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) {
-        const int col4 = gcol[c] * 16 + kq;
-        bias4[c] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
-        tp4[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
-                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    // tail tiles (TM_MFMA4): after the k-slice reduce-scatter lane l holds tail row l&3,
-    // column tcol of the tile
-    const int tcol = 4 * ((lane >> 2) & 3) + (lane >> 4);
-    float tbias[NQ], ttp[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        tbias[q] = 0.f;
-        ttp[q] = 0.f;
-        if constexpr (TM == TM_MFMA4) {
-            const int col = gcol[q] * 16 + tcol;
-            if (MODE != E_STORE_NB) tbias[q] = e.bias[col];
-            if (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ttp[q] = e.tproj[col];
-        }
-    }
-    const BSrc src = bsrc<NC, KB>(Bp, ct0, lane);
-    int soff[NCW];
-    tile_offsets<NCW, KB>(soff, src.sbase, rot);
-    // S-stage register ring: slot st holds k-block kb+st; its refill (k-block kb+st+S) is issued
-    // right after its MFMAs, so loads run S-1 slots ahead of use.  3 slots where a slot is
-    // short (NCW <= 6: 24-48 MFMAs, below the loaded L2 latency), 2 for the 9-tile QKV halves.
-    constexpr int S = (KB == 1) ? 1 : (NCW <= 6 && KB % 3 == 0) ? 3 : 2;
-    static_assert(KB == 1 || KB % S == 0, "ring slots divide the k-blocks");
-    static_assert(!XS2 || (S == 3 && KB > 2 * S && 2 * S * 16 == D), "XS2: the 96-wide x block is k-blocks 0..5");
-    f32x4 as[S][NR], ts[S][TA], bs[S][NCW];
-    f32x4 gs[S], ss[S];                         // LNA: gains / shifts of the slot's k's
-    // A k-block kb of slot st: from AX for kb < 2S (XS2), else from A
-    auto loadA = [&](int st, int kb) {
-        if (XS2 && kb < 2 * S) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) as[st][i] = *reinterpret_cast<const f32x4*>(AX + xoff[i] + kb * 16);
-            ts[st][0] = *reinterpret_cast<const f32x4*>(AX + xtoff + kb * 16);
-        } else {
-            g.loadA(as[st], ts[st], A, kb);
-        }
-    };
-    f32x2 nrm[NR], tnrm = {0.f, 0.f};           // LNA: (mean, 1/(std+eps)) of the lane's rows
-    if constexpr (LNA) {
-        static_assert(TM == TM_MFMA4, "fused LN operand: 4x4x1 tail rows");
-#pragma unroll
-        for (int i = 0; i < NR; ++i) nrm[i] = ln_row_norm(lst, (rt0 + i) * 16 + rl);
-        tnrm = ln_row_norm(lst, trow0 + (lane & 3));
-    }
-    auto loadLN = [&](int st, int kb) {
-        if constexpr (LNA) {
-            gs[st] = *reinterpret_cast<const f32x4*>(lg + kb * 16 + kq);
-            ss[st] = *reinterpret_cast<const f32x4*>(lb + kb * 16 + kq);
-        }
-    };
-    // LNA: slot st's operand is normalised one ring block ahead, between the previous slot's
-    // MFMAs (scalar VALU fills their issue gaps; packed f32 ops beside MFMAs cost more)
-    auto lnx = [&](int st) {
-        if constexpr (LNA) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int i = 0; i < NR; ++i) as[st][i][j] = fmaf((as[st][i][j] - nrm[i][0]) * nrm[i][1], gs[st][j], ss[st][j]);
-                ts[st][0][j] = fmaf((ts[st][0][j] - tnrm[0]) * tnrm[1], gs[st][j], ss[st][j]);
-            }
-        }
-    };
-    auto mma = [&](int st) {
-        g.mma(as[st], ts[st], bs[st]);
-        if constexpr (LNA) lnx(st + 1 < S ? st + 1 : 0);
-    };
-    auto mma_first = [&]() {
-        g.template mma<true>(as[0], ts[0], bs[0]);
-        if constexpr (LNA) lnx(S > 1 ? 1 : 0);
-    };
-    // residual epilogues: the wave's own output tiles of dst (its rows 64..67 columns too), read
-    // before the last ring pass so the epilogue waits on no LDS round trip (the GEMM's A operand
-    // is never dst, and no other wave writes these tiles before this wave's epilogue)
-    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
-    const int trow = trow0 + (lane & 3);
-    f32x4 old[NR][NCW];
-    float oldt[NQ];
-    auto load_old = [&]() {
-        if constexpr (RES) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-#pragma unroll
-                for (int c = 0; c < NCW; ++c)
-                    old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
-            if constexpr (TM == TM_MFMA4) {
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) oldt[q] = e.dst[min(trow, R - 1) * e.ldd + gcol[q] * 16 + tcol];
-            }
-        }
-    };
-#pragma unroll
-    for (int c = 0; c < NCW; ++c) {
-        bs[0][c] = pre.b0[c];
-        if constexpr (S > 1) bs[1][c] = pre.b1[c];
-    }
-    DPK_GEMM_HOOK(0);
-#pragma unroll
-    for (int st = 2; st < S; ++st) T::loadB(bs[st], src, soff, st);
-#pragma unroll
-    for (int st = 0; st < S; ++st) {
-        loadA(st, st);
-        loadLN(st, st);
-    }
-    lnx(0);
-    if constexpr (KB > S) {
-        // first ring pass peeled: its k-step 0 starts the accumulators from C = 0
-#pragma unroll
-        for (int st = 0; st < S; ++st) {
-            if (st == 0) mma_first();
-            else mma(st);
-            T::loadB(bs[st], src, soff, st + S);
-            loadA(st, st + S);
-            loadLN(st, st + S);
-            T::schedule_half();
-        }
-#pragma unroll 1
-        for (int kb = S; kb < KB - S; kb += S) {
-#pragma unroll
-            for (int st = 0; st < S; ++st) {
-                mma(st);
-                T::loadB(bs[st], src, soff, kb + st + S);
-                g.loadA(as[st], ts[st], A, kb + st + S);
-                loadLN(st, kb + st + S);
-                T::schedule_half();
-            }
-        }
-        load_old();
-#pragma unroll
-        for (int st = 0; st < S; ++st) {
-            g.mma(as[st], ts[st], bs[st]);
-            if (st + 1 < S) lnx(st + 1);
-        }
-    } else {
-        load_old();
-#pragma unroll
-        for (int st = 0; st < S; ++st) {
-            if (st == 0) g.template mma<true>(as[st], ts[st], bs[st]);
-            else g.mma(as[st], ts[st], bs[st]);
-            if (st + 1 < S) lnx(st + 1);
-        }
-    }
-    DPK_GEMM_HOOK(1);
-    auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
-        if constexpr (MODE != E_CHEB1) return f32x4{0.f, 0.f, 0.f, 0.f};
-        if (e.tproj_pose_stride == 0) return uniform4;
-        const int pose = min(e.pose0 + row / J, e.pose_max);
-        return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
-    };
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int row = (rt0 + i) * 16 + rl;
-        f32x4 vo[NCW];
-#pragma unroll
-        for (int c = 0; c < NCW; ++c) {
-            const int col4 = gcol[c] * 16 + kq;
-            const f32x4 tp = tproj4(row, col4, tp4[c]);
-            const f32x4 v = epi_value4<MODE>(g.acc[i][c], bias4[c], tp, RES ? old[i][c] : f32x4{0.f, 0.f, 0.f, 0.f});
-            *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
-            vo[c] = v;
-        }
-        if constexpr (STATS) {
-            // this row's 48 columns of the half: 12 in this lane, the rest in lanes l^16, l^32, l^48
-            static_assert(NCW == 3, "LayerNorm partials over 48-column halves");
-            const f32x4 s4 = (vo[0] + vo[1]) + vo[2];
-            const float mh = sum4rows((s4[0] + s4[1]) + (s4[2] + s4[3])) * (1.0f / 48.0f);
-            f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < NCW; ++c) {
-                const f32x4 d = vo[c] - mh;
-                q4 = __builtin_elementwise_fma(d, d, q4);
-            }
-            const float m2 = sum4rows((q4[0] + q4[1]) + (q4[2] + q4[3]));
-            if (lane < 16) *reinterpret_cast<f32x2*>(e.st + row * 4 + 2 * (ct0 / NCW)) = f32x2{mh, m2};
-        }
-    }
-    if constexpr (TM == TM_VALU) {
-        static_assert(TM != TM_VALU, "gemm_wave computes transposed tiles; VALU tails are gemm_out's");
-    } else if constexpr (TM == TM_MFMA4) {
-        // reduce-scatter the 4 k-slices: lane l then holds tail row l&3, column tcol of tile q
-        const int row = trow;
-        float tv[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const float v = rs4rows(g.tacc[q][0], g.tacc[q][1], g.tacc[q][2], g.tacc[q][3]);
-            tv[q] = 0.f;
-            if ((q == NQ - 1 && tail_dup) || row >= R) continue;   // dup tile / rows past R
-            const int col = gcol[q] * 16 + tcol;
-            float* dp = e.dst + row * e.ldd + col;
-            const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
-            tv[q] = epi_value<MODE>(v, tbias[q], tp, RES ? oldt[q] : 0.f);
-            *dp = tv[q];
-        }
-        if constexpr (STATS) {
-            // tail row l&3: this wave's valid tail tiles, 16 columns each, spread over the 16 lanes
-            // with that l&3 (lane bits 2-3 by DPP row rotation, bits 4-5 by permlane)
-            const int nq = (NQ - (tail_dup ? 1 : 0));
-            const float cnt = 16.0f * (float)nq;   // 32 (waves 0,1) or 16 (waves 2,3)
-            float sm = 0.f;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) sm += (q < nq) ? tv[q] : 0.f;
-            sm += row_ror<4>(sm);
-            sm += row_ror<8>(sm);
-            const float mt = sum4rows(sm) * (1.0f / 16.0f) * (nq == 2 ? 0.5f : 1.0f);
-            float sq = 0.f;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float d = tv[q] - mt;
-                sq += (q < nq) ? d * d : 0.f;
-            }
-            sq += row_ror<4>(sq);
-            sq += row_ror<8>(sq);
-            sq = sum4rows(sq);
-            const int wv = 2 * (rt0 / NR) + (ct0 / NCW);   // wave index (row pair, column half)
-            if (lane < 4 && row < R) *reinterpret_cast<f32x4*>(e.st + ST_TAIL + (lane * 4 + wv) * 4) = f32x4{cnt, mt, sq, 0.f};
-        }
-    }
-    DPK_GEMM_HOOK(2);
-}
-
-// Whole-workgroup GEMM with NC output col tiles.  Wave w (of 4): row tiles 2*(w>>1) and
-// 2*(w>>1)+1 and column half w&1 on the 16x16x4 MFMA; the 4 tail rows 64..67 of that column
-// half on 4x4x1 MFMAs, split between the half's two waves (rotated column order for w>>1 = 1).
-template <int NC, int KB, int MODE, bool STATS = false, bool LNA = false, bool XS2 = false>
-__device__ __forceinline__ void gemm_wg(const float* A, int lda, const float* Bp, int wave, int lane,
-                                        const EpiArgs& e, const BPre<NC / 2>& pre, const float* lst = nullptr,
-                                        const float* lg = nullptr, const float* lb = nullptr,
-                                        const float* AX = nullptr, int ldx = 0) {
-    static_assert(NC % 2 == 0 && (R == 68 || R == 34) && NW == 4, "row tiles x 2 column halves + tail rows");
-    constexpr int NCW = NC / 2;
-    constexpr int NRW = R == 68 ? 2 : 1;            // row tiles per wave
-    const int pr = gemm_pr(wave);
-    const bool dup = (NCW & 1) && pr == 1;
-    gemm_wave<NRW, NCW, TM_MFMA4, 0, NC, KB, MODE, STATS, LNA, XS2>(A, lda, Bp, NRW * pr, gemm_ch(wave) * NCW,
-                                                                    col_rot<NCW>(wave), R - R % 16, dup, lane, e,
-                                                                    pre, lst, lg, lb, AX, ldx);
-}
-
-// ---------------------------------------------------------------------------------------
-// Split-fp16 GEMM (gemm mode 1): out = A.W as 3 fp16 MFMA products per tile and k-block,
-// hi(A)hi(W) + hi(A)lo(W) + lo(A)hi(W), accumulated in fp32 (v_mfma_f32_16x16x32_f16; the
-// dropped lo.lo term is ~2^-22 relative).  fp16 x fp16 products are exact in fp32, so the error
-// is that of the two-part split: ~2^-22 per product (fp32 rounding: 2^-24).  5.3x the fp32 MFMA
-// rate (16 cycles per 16x16x32 vs 8 x 32 cycles for the same k on 16x16x4 f32).
-// Weights carry a x64 scale (exact power of two, undone in the epilogue) so their lo parts stay
-// normal fp16.  Same tile geometry as the fp32 path: transposed tiles, 4 tail rows on
-// v_mfma_f32_4x4x4_16b_f16 split between the two waves of a column half; columns in passes of
-// 3 tiles (keeps the hi+lo B ring within the register budget).
-struct BSrc16 {
-    __amdgpu_buffer_rsrc_t rsrc;
-    int voff;
-    __device__ __forceinline__ f16x8 load(int byteoff) const {
-        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, byteoff, 0));
-    }
-};
-template <int NC, int KB32>
-__device__ __forceinline__ BSrc16 bsrc16(const char* Bp, int lane) {
-    BSrc16 s;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, (short)0, NC * KB32 * BLK16, 0x00020000);
-    s.voff = lane * 16;
-    return s;
-}
-
-constexpr int PW16 = 3;      // column tiles per pass
-template <int PW>
-struct BPre16 {
-    f16x8 h0[PW], l0[PW], h1[PW], l1[PW];
-};
-
-// global column tile of local tile c of a pass starting at ctp, rotated by rot
-template <int PW>
-__device__ __forceinline__ int pass_col(int ctp, int c, int rot) {
-    const int cc = c + rot;
-    return ctp + (cc >= PW ? cc - PW : cc);
-}
-
-// first two k-blocks of the wave's first pass (issued before the preceding VALU phase)
-template <int G, int NC, int KB32>
-__device__ __forceinline__ BPre16<PW16> gemm16_prefetch(const char* Bp, int wave, int lane) {
-    constexpr int NCW = NC / 2;
-    const BSrc16 s = bsrc16<NC, KB32>(Bp, lane);
-    const int ctp = gemm_ch(wave) * NCW, rot = gemm_pr(wave) ? (PW16 + 1) / 2 : 0;
-    BPre16<PW16> pre;
-#pragma unroll
-    for (int c = 0; c < PW16; ++c) {
-        const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
-        pre.h0[c] = s.load(b0);
-        pre.h1[c] = s.load(b0 + BLK16);
-        if constexpr (G == 1) {
-            pre.l0[c] = s.load(b0 + 1024);
-            pre.l1[c] = s.load(b0 + BLK16 + 1024);
-        }
-    }
-    return pre;
-}
-
-__device__ __forceinline__ f16x4 half_lo(f16x8 v) { return __builtin_shufflevector(v, v, 0, 1, 2, 3); }
-__device__ __forceinline__ f16x4 half_hi(f16x8 v) { return __builtin_shufflevector(v, v, 4, 5, 6, 7); }
-
-template <int G, int NR, int PW, int NC, int KB32, int MODE, int OUTSPLIT>
-__device__ __forceinline__ void gemm16_pass(const char* A, int lda, const BSrc16& src, int rt0, int ctp, int rot,
-                                            int trow0, bool tail_dup, int lane, const EpiArgs& e,
-                                            const BPre16<PW>& pre) {
-    constexpr int NQ = (PW + 1) / 2;
-    lane = opaque(lane);
-    const int rl = lane & 15, g = lane >> 4, kq = g * 4;
-    int gcol[PW], soff[PW];
-#pragma unroll
-    for (int c = 0; c < PW; ++c) {
-        gcol[c] = pass_col<PW>(ctp, c, rot);
-        soff[c] = gcol[c] * KB32 * BLK16;
-    }
-    f32x4 bias4[PW], tp4[PW];
-    float tbias[NQ], ttp[NQ];
-    const int tcol = 4 * ((lane >> 2) & 3) + g;     // tail column of this lane after the reduce-scatter
-#pragma unroll
-    for (int c = 0; c < PW; ++c) {
-        const int col4 = gcol[c] * 16 + kq;
-        bias4[c] = MODE == E_STORE_NB ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(e.bias + col4);
-        tp4[c] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? *reinterpret_cast<const f32x4*>(e.tproj + col4)
-                                                               : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int col = gcol[q] * 16 + tcol;
-        tbias[q] = MODE == E_STORE_NB ? 0.f : e.bias[col];
-        ttp[q] = (MODE == E_CHEB1 && e.tproj_pose_stride == 0) ? e.tproj[col] : 0.f;
-    }
-    int aoff[NR];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) aoff[i] = ((rt0 + i) * 16 + rl) * lda + g * 32;
-    const int toff = (trow0 + (lane & 3)) * lda + g * 32;
-    f32x4 acc[NR][PW], tacc[NQ];
-#pragma unroll
-    for (int i = 0; i < NR; ++i)
-#pragma unroll
-        for (int c = 0; c < PW; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) tacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f16x8 bh[2][PW], bl[2][PW], ah[2][NR], al[2][NR], th[2], tl[2];
-#pragma unroll
-    for (int c = 0; c < PW; ++c) {
-        bh[0][c] = pre.h0[c];
-        bl[0][c] = pre.l0[c];
-        bh[1][c] = pre.h1[c];
-        bl[1][c] = pre.l1[c];
-    }
-    auto loadA = [&](int st, int kb) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            ah[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128);
-            if constexpr (G == 1) al[st][i] = *reinterpret_cast<const f16x8*>(A + aoff[i] + kb * 128 + 16);
-        }
-        th[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128);
-        if constexpr (G == 1) tl[st] = *reinterpret_cast<const f16x8*>(A + toff + kb * 128 + 16);
-    };
-    loadA(0, 0);
-    if constexpr (KB32 > 1) loadA(1, 1);
-#pragma unroll
-    for (int kb = 0; kb < KB32; ++kb) {
-        const int st = kb & 1;
-        // transposed tiles: weight fragment as the A operand (cf. GemmTile TRANS)
-        if constexpr (G == 2) {
-            // bf16 (gemm mode 2): one product per tile, hi halves only
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-#pragma unroll
-                for (int c = 0; c < PW; ++c)
-                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bh[st][c]),
-                                                                        __builtin_bit_cast(bf16x8, ah[st][i]), acc[i][c], 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(__builtin_bit_cast(s16x4, half_lo(bh[st][q])),
-                                                                 __builtin_bit_cast(s16x4, half_lo(th[st])), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4bf16_1k(__builtin_bit_cast(s16x4, half_hi(bh[st][q])),
-                                                                 __builtin_bit_cast(s16x4, half_hi(th[st])), tacc[q], 0, 0, 0);
-            }
-        } else {
-    #pragma unroll
-            for (int i = 0; i < NR; ++i)
-    #pragma unroll
-                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl[st][c], ah[st][i], acc[i][c], 0, 0, 0);
-    #pragma unroll
-            for (int i = 0; i < NR; ++i)
-    #pragma unroll
-                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], al[st][i], acc[i][c], 0, 0, 0);
-    #pragma unroll
-            for (int i = 0; i < NR; ++i)
-    #pragma unroll
-                for (int c = 0; c < PW; ++c) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh[st][c], ah[st][i], acc[i][c], 0, 0, 0);
-    #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bl[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bl[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(tl[st]), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(tl[st]), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_lo(bh[st][q]), half_lo(th[st]), tacc[q], 0, 0, 0);
-                tacc[q] = __builtin_amdgcn_mfma_f32_4x4x4f16(half_hi(bh[st][q]), half_hi(th[st]), tacc[q], 0, 0, 0);
-            }
-}
-        if (kb + 2 < KB32) {
-#pragma unroll
-            for (int c = 0; c < PW; ++c) {
-                bh[st][c] = src.load(soff[c] + (kb + 2) * BLK16);
-                if constexpr (G == 1) bl[st][c] = src.load(soff[c] + (kb + 2) * BLK16 + 1024);
-            }
-            loadA(st, kb + 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    DPK_GEMM_HOOK(1);
-    constexpr bool RES = MODE == E_RESID || MODE == E_RESID_RELU;
-    constexpr float INV = 1.0f / W16_SCALE;
-    auto tproj4 = [&](int row, int col4, const f32x4& uniform4) -> f32x4 {
-        if constexpr (MODE != E_CHEB1) return f32x4{0.f, 0.f, 0.f, 0.f};
-        if (e.tproj_pose_stride == 0) return uniform4;
-        const int pose = min(e.pose0 + row / J, e.pose_max);
-        return *reinterpret_cast<const f32x4*>(e.tproj + (size_t)pose * e.tproj_pose_stride + col4);
-    };
-    auto store = [&](int row, int col4, const f32x4& v) {
-        if constexpr (OUTSPLIT) split_store4<OUTSPLIT>(reinterpret_cast<char*>(e.dst + row * e.ldd), col4, v);
-        else *reinterpret_cast<f32x4*>(e.dst + row * e.ldd + col4) = v;
-    };
-    f32x4 old[NR][PW];
-    if constexpr (RES) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int c = 0; c < PW; ++c)
-                old[i][c] = *reinterpret_cast<const f32x4*>(e.dst + ((rt0 + i) * 16 + rl) * e.ldd + gcol[c] * 16 + kq);
-    }
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int row = (rt0 + i) * 16 + rl;
-#pragma unroll
-        for (int c = 0; c < PW; ++c) {
-            const int col4 = gcol[c] * 16 + kq;
-            const f32x4 tp = tproj4(row, col4, tp4[c]);
-            f32x4 v;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                v[r] = epi_value<MODE>(acc[i][c][r] * INV, bias4[c][r], tp[r], RES ? old[i][c][r] : 0.f);
-            store(row, col4, v);
-        }
-    }
-    const int row = trow0 + (lane & 3);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const float v = rs4rows(tacc[q][0], tacc[q][1], tacc[q][2], tacc[q][3]);
-        if ((q == NQ - 1 && tail_dup) || row >= R) continue;
-        const int col = gcol[q] * 16 + tcol;
-        const float oldt = RES ? e.dst[row * e.ldd + col] : 0.f;
-        const float tp = MODE == E_CHEB1 ? tproj_at(e, row, col, ttp[q]) : 0.f;
-        const float o = epi_value<MODE>(v * INV, tbias[q], tp, oldt);
-        if constexpr (OUTSPLIT) split_store1<OUTSPLIT>(reinterpret_cast<char*>(e.dst + row * e.ldd), col, o);
-        else e.dst[row * e.ldd + col] = o;
-    }
-    DPK_GEMM_HOOK(2);
-}
-
-// Whole-workgroup split-fp16 GEMM: same wave roles as gemm_wg; the wave's NC/2 column tiles in
-// passes of PW16.  A: split rows (bytes, stride lda); B: this GEMM's split weight blocks.
-template <int G, int NC, int KB32, int MODE, int OUTSPLIT>
-__device__ __forceinline__ void gemm_wg16(const char* A, int lda, const char* Bp, int wave, int lane,
-                                          const EpiArgs& e, const BPre16<PW16>& pre) {
-    static_assert(NC % 2 == 0 && (NC / 2) % PW16 == 0 && (R == 68 || R == 34), "passes of 3 column tiles");
-    constexpr int NCW = NC / 2, NRW = R == 68 ? 2 : 1, NPASS = NCW / PW16;
-    const int pr = gemm_pr(wave);
-    const int rot = pr ? (PW16 + 1) / 2 : 0;
-    const bool dup = (PW16 & 1) && pr == 1;
-    const BSrc16 src = bsrc16<NC, KB32>(Bp, lane);
-    DPK_GEMM_HOOK(0);
-    gemm16_pass<G, NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, gemm_ch(wave) * NCW, rot, R - R % 16, dup,
-                                                     lane, e, pre);
-#pragma unroll 1
-    for (int ps = 1; ps < NPASS; ++ps) {
-        const int ctp = gemm_ch(wave) * NCW + ps * PW16;
-        BPre16<PW16> p2;
-#pragma unroll
-        for (int c = 0; c < PW16; ++c) {
-            const int b0 = pass_col<PW16>(ctp, c, rot) * KB32 * BLK16;
-            p2.h0[c] = src.load(b0);
-            p2.h1[c] = src.load(b0 + BLK16);
-            if constexpr (G == 1) {
-                p2.l0[c] = src.load(b0 + 1024);
-                p2.l1[c] = src.load(b0 + BLK16 + 1024);
-            }
-        }
-        gemm16_pass<G, NRW, PW16, NC, KB32, MODE, OUTSPLIT>(A, lda, src, NRW * pr, ctp, rot, R - R % 16, dup, lane, e, p2);
-    }
-}
-
-// Output ChebConv (96->5, one col tile): waves 0-3, wave w = row tile w + tail row 64+w; the
-// raw accumulators go to a functor (DDIM update).
-template <int KB>
-__device__ __forceinline__ BPre<1> out_prefetch(const float* Bp, int lane) {
-    const BSrc s = bsrc<1, KB>(Bp, 0, lane);
-    BPre<1> pre;
-    pre.b0[0] = s.load(0);
-    pre.b1[0] = s.load(1);
-    return pre;
-}
-
-template <int KB, int NCOL, class Epi>
-__device__ __forceinline__ void gemm_out(const float* A, int lda, const float* Bp, int wave, int lane, Epi epi,
-                                         const BPre<1>& pre) {
-    using T = GemmTile<1, 1, TM_VALU, 1, KB, false>;
-    static_assert(KB % 2 == 0, "k-blocks in pairs");
-    lane = opaque(lane);
-    T g;
-    g.acc[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g.tl[0][0] = 0.f;
-    const int rl = lane & 15, kq = (lane >> 4) * 4;
-    g.aoff[0] = (wave * 16 + rl) * lda + kq;
-    g.toff[0] = (R - R % 16 + wave) * lda + kq;
-    const BSrc src = bsrc<1, KB>(Bp, 0, lane);
-    const int soff[1] = {0};
-    f32x4 a0[1], t0[1], b0[1] = {pre.b0[0]}, a1[1], t1[1], b1[1] = {pre.b1[0]};
-    g.loadA(a0, t0, A, 0);
-    g.loadA(a1, t1, A, 1);
-#pragma unroll 1
-    for (int kb = 0; kb < KB - 2; kb += 2) {
-        g.mma(a0, t0, b0);
-        T::loadB(b0, src, soff, kb + 2);
-        g.loadA(a0, t0, A, kb + 2);
-        g.mma(a1, t1, b1);
-        T::loadB(b1, src, soff, kb + 3);
-        g.loadA(a1, t1, A, kb + 3);
-    }
-    g.mma(a0, t0, b0);
-    g.mma(a1, t1, b1);
-    const float tv = sum4rows(g.tl[0][0]);
-    if (rl < NCOL) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) epi(wave * 16 + kq + r, rl, g.acc[0][0][r]);
-        if (kq == 0) epi(R - R % 16 + wave, rl, tv);
-    }
-}
-// ---------------------------------------------------------------------------------------
-// Correctly rounded x / d from a shared reciprocal r = 1/d (Markstein: one fma residual
-// correction).  Used where a whole row is divided by one value (LayerNorm).
-__device__ __forceinline__ float div_by(float x, float d, float r) {
-    const float q = x * r;
-    const float e = fmaf(-q, d, x);
-    return fmaf(e, r, q);
-}
-
-// DPP row (16-lane) all-reduces (row_ror: before sum4rows)
-// all-reduce over the 16 lanes of a DPP row
-__device__ __forceinline__ float row_max(float v) {
-    v = fmaxf(v, row_ror<8>(v));
-    v = fmaxf(v, row_ror<4>(v));
-    v = fmaxf(v, row_ror<2>(v));
-    return fmaxf(v, row_ror<1>(v));
-}
-__device__ __forceinline__ float row_sum(float v) {
-    v += row_ror<8>(v);
-    v += row_ror<4>(v);
-    v += row_ror<2>(v);
-    return v + row_ror<1>(v);
-}
-
-// LayerNorm of GraFormer (GraFormer.py:58-70): a*(x-mean)/(std_unbiased + eps) + b.
-// Rows 0..63: a DPP quad (4 lanes) per row, 16 rows per wave; lane `part` of a row owns the
-// 16-byte chunks part, part+4, ..., part+20 (interleaved across LDS banks).  Rows 64..67: wave w
-// takes row 64+w, 16 lanes x 6 elements (columns 2*lane + 32*e), lanes 16..63 mirror 0..15.
-// One-pass fp32 statistics shifted by the row's first element (below); the cross-lane sums are
-// DPP all-reduces whose operands pair up commutatively, so every lane of a row holds bitwise the
-// same mean/std.  The division by the row's std+eps is correctly rounded (div_by with a
-// Newton-refined reciprocal), as the reference's true division.
-__device__ __forceinline__ float quad_sum(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
-                                                               0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
-                                                                     0x4E, 0xf, 0xf, false));   // [2,3,0,1]
-}
-__device__ __forceinline__ f32x4 div_by4(f32x4 x, float d, float r) {
-    const f32x4 q = x * r;
-    const f32x4 e = __builtin_elementwise_fma(-q, f32x4{d, d, d, d}, x);
-    return __builtin_elementwise_fma(e, f32x4{r, r, r, r}, q);
-}
-__device__ __forceinline__ f32x2 div_by2(f32x2 x, float d, float r) {
-    const f32x2 q = x * r;
-    const f32x2 e = __builtin_elementwise_fma(-q, f32x2{d, d}, x);
-    return __builtin_elementwise_fma(e, f32x2{r, r}, q);
-}
-template <int SPLIT = 0>
-__device__ __forceinline__ void layer_norm(const float* src, float* dst, const float* gain, const float* shift,
-                                           int tid) {
-    tid = opaque(tid);
-    const int w = tid >> 6, lane = tid & 63;
-    constexpr float RD = 1.0f / (float)D, RD1 = 1.0f / (float)(D - 1);
-    // ---- rows 0..63: wave w rows 16w..16w+15; row 64 + w: the tail row of wave w
-    constexpr int RM = R - R % 16, RT = R % 16;
-    static_assert(RM == 64 && RT == NW, "4 row tiles + one tail row per wave");
-    const int row = w * 16 + (lane >> 2), part = lane & 3;
-    const float* s = src + row * LDX;
-    const int tl = lane & 15;
-    const float* st = src + (RM + w) * LDX;
-    // the row chunks, and the gains/shifts of the lane's columns, all issued up front: the
-    // normalisation then waits on no LDS round trip (one per chunk when they were read there)
-    f32x4 v[6], gv[6], sv[6];
-    f32x2 u[3], tg[3], tsh[3];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) v[e] = *reinterpret_cast<const f32x4*>(s + 4 * (part + 4 * e));
-#pragma unroll
-    for (int e = 0; e < 3; ++e) u[e] = *reinterpret_cast<const f32x2*>(st + 2 * tl + 32 * e);
-    const float c0 = s[0], tc0 = st[0];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-        gv[e] = *reinterpret_cast<const f32x4*>(gain + 4 * (part + 4 * e));
-        sv[e] = *reinterpret_cast<const f32x4*>(shift + 4 * (part + 4 * e));
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        tg[e] = *reinterpret_cast<const f32x2*>(gain + 2 * tl + 32 * e);
-        tsh[e] = *reinterpret_cast<const f32x2*>(shift + 2 * tl + 32 * e);
-    }
-    // One pass over the row, shifted by its first element c0 (every lane of the row reads the same
-    // value): S1 = sum(x - c0), S2 = sum((x - c0)^2); mean = c0 + S1/96, var = (S2 - S1^2/96)/95
-    // (unbiased, GraFormer.py:64).  With the shift inside the row's range the two sums stay of the
-    // order of the variance, so the one-pass form loses nothing measurable against the two-pass
-    // one, and the two reductions share one DPP chain.
-    f32x4 d1 = {0.f, 0.f, 0.f, 0.f}, d2 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-        const f32x4 d = v[e] - c0;
-        d1 += d;
-        d2 = __builtin_elementwise_fma(d, d, d2);
-    }
-    f32x2 e1 = {0.f, 0.f}, e2 = {0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        const f32x2 d = u[e] - tc0;
-        e1 += d;
-        e2 = __builtin_elementwise_fma(d, d, e2);
-    }
-    const float s1 = quad_sum((d1[0] + d1[1]) + (d1[2] + d1[3]));
-    const float s2 = quad_sum((d2[0] + d2[1]) + (d2[2] + d2[3]));
-    const float t1 = row_sum(e1[0] + e1[1]);
-    const float t2 = row_sum(e2[0] + e2[1]);
-    const float mean = fmaf(s1, RD, c0), tmean = fmaf(t1, RD, tc0);
-    const float var = fmaxf(fmaf(-s1 * RD, s1, s2), 0.f) * RD1;
-    const float tvar = fmaxf(fmaf(-t1 * RD, t1, t2), 0.f) * RD1;
-    const float den = __builtin_amdgcn_sqrtf(var) + LN_EPS, tden = __builtin_amdgcn_sqrtf(tvar) + LN_EPS;   // v_sqrt_f32 (1 ulp)
-    const float rcp = rcp_nr(den), trcp = rcp_nr(tden);
-    float* d = dst + row * LDX;
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-        const int c = 4 * (part + 4 * e);
-        const f32x4 t = div_by4(gv[e] * (v[e] - mean), den, rcp) + sv[e];
-        if constexpr (SPLIT) split_store4<SPLIT>(reinterpret_cast<char*>(d), c, t);
-        else *reinterpret_cast<f32x4*>(d + c) = t;
-    }
-    // the tail row: lanes 16..63 mirror 0..15 and store nothing
-    float* dt = dst + (RM + w) * LDX;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-        const int c = 2 * tl + 32 * e;
-        const f32x2 t = div_by2(tg[e] * (u[e] - tmean), tden, trcp) + tsh[e];
-        if (lane < 16) {
-            if constexpr (SPLIT) split_store2<SPLIT>(reinterpret_cast<char*>(dt), c, t);
-            else *reinterpret_cast<f32x2*>(dt + c) = t;
-        }
-    }
-}
-
-// 4-head attention over the 17 joints of each pose (GraFormer.py:99-140, without the
-// projections).  One DPP row (16 lanes) per (pose, head); lane q owns query q AND key/value
-// row q in registers.  Keys/values 0..15 reach the other lanes of the row by DPP row_newbcast
-// fused into the FMA (v_fmac_f32_dpp), so the K/V rows are read from LDS once per lane instead
-// of once per (query, key).  Row 16 (key/value 16) is read by every lane of the row; query 16
-// is computed cooperatively (lane j scores key j; lane q sums value column q over the keys).
-template <int J>
-__device__ __forceinline__ void fmac_bcast(float& acc, float row_src, float x) {
-    // acc += row_src[lane J of this 16-lane row] * x
-    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-        : "+v"(acc)
-        : "v"(row_src), "v"(x), "i"(J));
-}
-
-// one feature d of this lane's query against keys 0..15 (key rows broadcast from their owner
-// lanes); 16 independent accumulators per instruction group
-template <int J>
-__device__ __forceinline__ void score_keys_d(float (&sc)[16], float kd, float qd) {
-    fmac_bcast<J>(sc[J], kd, qd);
-    if constexpr (J + 1 < 16) score_keys_d<J + 1>(sc, kd, qd);
-}
-template <int J>
-__device__ __forceinline__ void pv_keys(float (&o)[DK], const float (&vr)[DK], const float (&p)[17]) {
-#pragma unroll
-    for (int d = 0; d < DK; ++d) fmac_bcast<J>(o[d], vr[d], p[J]);
-    if constexpr (J + 1 < 16) pv_keys<J + 1>(o, vr, p);
-}
-template <int J>
-__device__ __forceinline__ void pv16_keys(float& o, float pj_row, const float* vcol) {
-    fmac_bcast<J>(o, pj_row, vcol[J * LD2]);
-    if constexpr (J + 1 < 16) pv16_keys<J + 1>(o, pj_row, vcol);
-}
-
-template <int SPLIT = 0>
-__device__ __forceinline__ void attention(const float* qkv, float* out, unsigned mask, int tid) {
-    tid = opaque(tid);
-    const int grp = tid >> 4, q = tid & 15;
-    const int p = grp >> 2, h = grp & 3;
-    if (p >= P) return;                                 // whole DPP rows (34-row tiles: waves 2-3)
-    const float* rows = qkv + p * J * LD2 + h * DK;     // row i: + i*LD2; K at +D, V at +2D
-    float* orows = out + p * J * LDX + h * DK;
-    const float rcp_sdk = 1.0f / SQRT_DK;
-    auto keyok = [&](int j) { return ((mask >> j) & 1u) != 0u; };
-    float qr[DK], kr[DK], vr[DK], k16[DK], v16[DK];
-#pragma unroll
-    for (int d = 0; d < DK; d += 4) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(rows + q * LD2 + d);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(rows + q * LD2 + D + d);
-        const f32x4 c = *reinterpret_cast<const f32x4*>(rows + q * LD2 + 2 * D + d);
-        const f32x4 e = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + D + d);
-        const f32x4 f = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + 2 * D + d);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            qr[d + i] = a[i];
-            kr[d + i] = b[i];
-            vr[d + i] = c[i];
-            k16[d + i] = e[i];
-            v16[d + i] = f[i];
-        }
-    }
-    // ---- query q: scores (scaled by division, GraFormer.py:104), softmax, P.V
-    float sc[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sc[j] = 0.f;
-#pragma unroll
-    for (int d = 0; d < DK; ++d) score_keys_d<0>(sc, kr[d], qr[d]);
-    float s16 = 0.f;
-#pragma unroll
-    for (int d = 0; d < DK; ++d) s16 = fmaf(qr[d], k16[d], s16);
-    float pr[17];
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const float dot = j < 16 ? sc[j] : s16;
-        pr[j] = keyok(j) ? div_by(dot, SQRT_DK, rcp_sdk) : -1e9f;
-        m = fmaxf(m, pr[j]);
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        pr[j] = expf(pr[j] - m);
-        sum += pr[j];
-    }
-    const float rs = 1.0f / sum;
-#pragma unroll
-    for (int j = 0; j < 17; ++j) pr[j] = div_by(pr[j], sum, rs);
-    float o[DK];
-#pragma unroll
-    for (int d = 0; d < DK; ++d) o[d] = 0.f;
-    pv_keys<0>(o, vr, pr);
-#pragma unroll
-    for (int d = 0; d < DK; ++d) o[d] = fmaf(pr[16], v16[d], o[d]);
-#pragma unroll
-    for (int d = 0; d < DK; d += 4)
-        if constexpr (SPLIT)
-            split_store4<SPLIT>(reinterpret_cast<char*>(out + (p * J + q) * LDX), h * DK + d, f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]});
-        else
-            *reinterpret_cast<f32x4*>(orows + q * LDX + d) = f32x4{o[d], o[d + 1], o[d + 2], o[d + 3]};
-    // ---- query 16: lane j scores key j (its own key row); key 16 by every lane
-    {
-        float a16 = 0.f, b16 = 0.f;
-#pragma unroll
-        for (int d = 0; d < DK; d += 4) {
-            const f32x4 qv = *reinterpret_cast<const f32x4*>(rows + 16 * LD2 + d);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a16 = fmaf(qv[i], kr[d + i], a16);
-                b16 = fmaf(qv[i], k16[d + i], b16);
-            }
-        }
-        const float sq = keyok(q) ? div_by(a16, SQRT_DK, rcp_sdk) : -1e9f;
-        const float sk = keyok(16) ? div_by(b16, SQRT_DK, rcp_sdk) : -1e9f;
-        const float mm = fmaxf(row_max(sq), sk);
-        const float eq = expf(sq - mm), ek = expf(sk - mm);
-        const float ss = row_sum(eq) + ek;
-        const float rss = 1.0f / ss;
-        const float pq = div_by(eq, ss, rss), pk = div_by(ek, ss, rss);
-        // dims q and q+16 of query 16's output: sum_j p_j * V[j][d] with V read from LDS
-        const float* vcol = rows + 2 * D;
-        float o0 = 0.f, o1 = 0.f;
-        asm volatile("s_nop 1" ::: "memory");   // VALU write of pq -> DPP read (2 wait states)
-        pv16_keys<0>(o0, pq, vcol + q);
-        o0 = fmaf(pk, vcol[16 * LD2 + q], o0);
-        char* row16 = reinterpret_cast<char*>(out + (p * J + 16) * LDX);
-        if constexpr (SPLIT) split_store1<SPLIT>(row16, h * DK + q, o0);
-        else orows[16 * LDX + q] = o0;
-        // all 16 lanes take part (the DPP broadcasts read every lane of the row); lanes q >= 8
-        // read columns past the head (inside the row) and discard them
-        pv16_keys<0>(o1, pq, vcol + q + 16);
-        o1 = fmaf(pk, vcol[16 * LD2 + q + 16], o1);
-        if (q < DK - 16) {
-            if constexpr (SPLIT) split_store1<SPLIT>(row16, h * DK + q + 16, o1);
-            else orows[16 * LDX + q + 16] = o1;
-        }
-    }
-}
-
-// Max over the 4 lane rows (l, l^16, l^32, l^48), result in every lane (cf. sum4rows).
-__device__ __forceinline__ float max4rows(float v) {
-    float a = v, b = v;
-    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    const float s1 = fmaxf(a, b);
-    float c = s1, d = s1;
-    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(c), "+v"(d));
-    return fmaxf(c, d);
-}
-
-// The same attention on the matrix cores (v_mfma_f32_16x16x4_f32).  Wave w = pose w, the 4
-// heads in turn.  Lane (g = l>>4, c = l&15) loads query/key row c at its 6 feature dims
-// {4g..4g+3, 16+2g, 17+2g}, the k-slice it feeds to the MFMAs, so:
-//   scores   S^T = K Q^T   (6 MFMAs): lane (g, c) ends with S[query c][keys 4g..4g+3];
-//   key 16 / query 16      per-lane partial dot products over the lane's dims, summed over
-//                          the 4 lane rows (permlane), so lane (g, c) also holds S[c][16],
-//                          S[16][c] and S[16][16];
-//   softmax  per query c: its 4 keys in registers, max/sum over the lane rows by permlane;
-//   P.V      O^T = V^T P^T (4 MFMAs per 16-wide column tile; lane row g feeds keys 4g..4g+3,
-//            the permuted order the scores left them in), so lane (g, c) ends with
-//            O[query c][dims 4g..4g+3] of the tile: one 16-byte store; key 16 added by FMA;
-//   query 16 lane (g, c) forms p16[c] * V[c][6g..6g+5], summed over the DPP row.
-// The reference's arithmetic (scores / sqrt(d_k), masked keys -1e9, softmax, P.V) in fp32, with
-// the scale taken as one multiply by log2(e)/sqrt(d_k) and exp(x) as 2^x (v_exp_f32): the
-// softmax is invariant to the base, so only roundings and summation orders differ.
-template <int SPLIT = 0>
-__device__ __forceinline__ void attention_mma(const float* qkv, float* out, unsigned mask, int wave, int lane) {
-    lane = opaque(lane);
-    if (wave >= P) return;
-    const int g = lane >> 4, c = lane & 15;
-    constexpr float LOG2E = 1.4426950408889634f;
-    const float sl = (1.0f / SQRT_DK) * LOG2E;      // scores in log2 units: exp(s/sqrt(dk)) = 2^(dot*sl)
-    const float* prow = qkv + wave * J * LD2;
-    float* orow = out + wave * J * LDX;
-    const bool kok16 = ((mask >> 16) & 1u) != 0u;
-    bool kokr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kokr[r] = ((mask >> (4 * g + r)) & 1u) != 0u;
-    // scores / sqrt(d_k), masked keys -1e9 (GraFormer.py:104-106), kept in log2 units (scaled by
-    // log2 e with the 1/sqrt(d_k)) so the softmax's exp is one v_exp_f32 (2^x) of (score - max) <= 0
-    auto scale = [&](float dot, bool ok) { return ok ? dot * sl : -1e9f; };
-    auto ex = [&](float x) { return __builtin_amdgcn_exp2f(x); };
-    // The 4 heads are independent: every stage below runs over all of them before the next
-    // stage, so the in-order issue interleaves 4 dependency chains (MFMA accumulations,
-    // permlane reductions, exp) instead of waiting out one head's latencies at a time.
-    f32x4 q4[NH], k4[NH], Q4[NH], K4[NH], V4a[NH], V4b[NH];
-    f32x2 q2[NH], k2[NH], Q2[NH], K2[NH];
-    float va[NH][4], vb[NH][4];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const float* rc = prow + h * DK + c * LD2;
-        const float* r16 = prow + h * DK + 16 * LD2;
-        q4[h] = *reinterpret_cast<const f32x4*>(rc + 4 * g);
-        q2[h] = *reinterpret_cast<const f32x2*>(rc + 16 + 2 * g);
-        k4[h] = *reinterpret_cast<const f32x4*>(rc + D + 4 * g);
-        k2[h] = *reinterpret_cast<const f32x2*>(rc + D + 16 + 2 * g);
-        Q4[h] = *reinterpret_cast<const f32x4*>(r16 + 4 * g);
-        Q2[h] = *reinterpret_cast<const f32x2*>(r16 + 16 + 2 * g);
-        K4[h] = *reinterpret_cast<const f32x4*>(r16 + D + 4 * g);
-        K2[h] = *reinterpret_cast<const f32x2*>(r16 + D + 16 + 2 * g);
-    }
-    // ---- scores S^T = K Q^T and, with query 16's row broadcast to every column,
-    //      S16 = K q16 (6 MFMAs each per head): lane (g, c) holds S[c][4g+r] and S[16][4g+r]
-    f32x4 st[NH], st16[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        st[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-        st16[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int m = 0; m < 6; ++m)
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            const float kk = m < 4 ? k4[h][m & 3] : k2[h][m & 1];
-            st[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? q4[h][m & 3] : q2[h][m & 1], st[h], 0, 0, 0);
-            st16[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk, m < 4 ? Q4[h][m & 3] : Q2[h][m & 1], st16[h], 0, 0, 0);
-        }
-    // V operands: column tile 0 (dims 0..15) and 1 (dims 16..23 in rows c < 8, ones in rows
-    // c >= 8: those rows of P.V come out as the softmax denominators, below)
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const float* vbase = prow + h * DK + 2 * D;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            va[h][r] = vbase[(4 * g + r) * LD2 + c];
-            const float v1 = vbase[(4 * g + r) * LD2 + 16 + (c & 7)];   // unconditional load, then select
-            vb[h][r] = c < 8 ? v1 : 1.0f;
-        }
-        V4a[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 4 * g);
-        V4b[h] = *reinterpret_cast<const f32x4*>(vbase + 16 * LD2 + 16 + 4 * (g & 1));
-    }
-    // ---- key 16 by partial dots over this lane's 6 dims, summed over the lane rows:
-    //      S[c][16] and S[16][16]
-    float s_c16[NH], s_1616[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        float pa = 0.f, pc = 0.f;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            pa = fmaf(q4[h][m], K4[h][m], pa);
-            pc = fmaf(Q4[h][m], K4[h][m], pc);
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            pa = fmaf(q2[h][m], K2[h][m], pa);
-            pc = fmaf(Q2[h][m], K2[h][m], pc);
-        }
-        s_c16[h] = pa;
-        s_1616[h] = pc;
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        s_c16[h] = scale(sum4rows(s_c16[h]), kok16);
-        s_1616[h] = scale(sum4rows(s_1616[h]), kok16);
-    }
-    // ---- softmax of query c and of query 16 over keys 4g+r (this lane) and 16
-    float p[NH][4], p16[NH], u[NH][4], u16[NH], mx[NH], my[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            p[h][r] = scale(st[h][r], kokr[r]);
-            u[h][r] = scale(st16[h][r], kokr[r]);
-        }
-        mx[h] = fmaxf(fmaxf(p[h][0], p[h][1]), fmaxf(p[h][2], p[h][3]));
-        my[h] = fmaxf(fmaxf(u[h][0], u[h][1]), fmaxf(u[h][2], u[h][3]));
-    }
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        mx[h] = fmaxf(max4rows(mx[h]), s_c16[h]);
-        my[h] = fmaxf(max4rows(my[h]), s_1616[h]);
-    }
-    // unnormalised probabilities; the denominators come out of the P.V products (ones rows)
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            p[h][r] = ex(p[h][r] - mx[h]);
-            u[h][r] = ex(u[h][r] - my[h]);
-        }
-        p16[h] = ex(s_c16[h] - mx[h]);
-        u16[h] = ex(s_1616[h] - my[h]);
-    }
-    // ---- O^T = V^T P^T over keys 0..15 (4 MFMAs per column tile), then key 16 by FMA;
-    //      query 16: this lane's keys 4g+r against V columns c and 16+c, summed over lane rows
-    f32x4 oa[NH], ob[NH];
-    float ya[NH], yb[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        oa[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ob[h] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ya[h] = 0.f;
-        yb[h] = 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-            oa[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[h][r], p[h][r], oa[h], 0, 0, 0);
-            ob[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(vb[h][r], p[h][r], ob[h], 0, 0, 0);
-            ya[h] = fmaf(u[h][r], va[h][r], ya[h]);
-            yb[h] = fmaf(u[h][r], vb[h][r], yb[h]);
-        }
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        ya[h] = sum4rows(ya[h]);
-        yb[h] = sum4rows(yb[h]);
-    }
-    // denominators: query c's over keys 0..15 sits in ob rows 8..15 (lane rows g >= 2), moved to
-    // lane rows 0,1 by one permlane32 swap; query 16's over keys 0..15 is yb of lanes c >= 8,
-    // moved to lanes c < 8 of the DPP row by a rotation by 8; key 16 added to both
-    float rs[NH], rs16[NH];
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        float sa = ob[h][0], sb = ob[h][0];
-        asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(sa), "+v"(sb));
-        const float den = (g < 2 ? sb : ob[h][0]) + p16[h];
-        const float yr = row_ror<8>(yb[h]);
-        const float den16 = (c < 8 ? yr : yb[h]) + u16[h];
-        rs[h] = __builtin_amdgcn_rcpf(den);
-        rs16[h] = __builtin_amdgcn_rcpf(den16);
-    }
-    // ---- stores: O[c][h*24 + 4g..] (tile 0), O[c][h*24 + 16 + 4g..] (tile 1, g < 2);
-    //      O[16][h*24 + c] and O[16][h*24 + 16 + c] (c < 8) from lane row 0
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-        const f32x4 p4 = {p16[h], p16[h], p16[h], p16[h]};
-        oa[h] = __builtin_elementwise_fma(p4, V4a[h], oa[h]) * rs[h];
-        ob[h] = __builtin_elementwise_fma(p4, V4b[h], ob[h]) * rs[h];
-        const float* v16 = prow + h * DK + 16 * LD2 + 2 * D;
-        const int col = h * DK;
-        if constexpr (SPLIT) {
-            char* rowc = reinterpret_cast<char*>(orow + c * LDX);
-            char* row16 = reinterpret_cast<char*>(orow + 16 * LDX);
-            split_store4<SPLIT>(rowc, col + 4 * g, oa[h]);
-            if (g < 2) split_store4<SPLIT>(rowc, col + 16 + 4 * g, ob[h]);
-            if (g == 0) split_store1<SPLIT>(row16, col + c, fmaf(u16[h], v16[c], ya[h]) * rs16[h]);
-            if (g == 1 && c < 8) split_store1<SPLIT>(row16, col + 16 + c, fmaf(u16[h], v16[16 + c], yb[h]) * rs16[h]);
-        } else {
-            *reinterpret_cast<f32x4*>(orow + c * LDX + col + 4 * g) = oa[h];
-            if (g < 2) *reinterpret_cast<f32x4*>(orow + c * LDX + col + 16 + 4 * g) = ob[h];
-            if (g == 0) orow[16 * LDX + col + c] = fmaf(u16[h], v16[c], ya[h]) * rs16[h];
-            if (g == 1 && c < 8) orow[16 * LDX + col + 16 + c] = fmaf(u16[h], v16[16 + c], yb[h]) * rs16[h];
-        }
-    }
-}
-
-// --- graph products -------------------------------------------------------------------
-// Chebyshev terms T1 = L, T2 = 2L^2 - I of the H36M skeleton (runners/diffpose_frame.py:120-124)
-// are sparse (49 / 87 of 289 entries).  Their pattern is derived here at compile time from the
-// edge list; dpk_set_graph() checks a given adjacency against it and packs the nonzero values
-// (row-major over the pattern) — any other graph runs the dense path.
-constexpr int H36M_EDGES[16][2] = {{0, 1}, {1, 2}, {2, 3}, {0, 4}, {4, 5}, {5, 6}, {0, 7}, {7, 8},
-                                   {8, 9}, {9, 10}, {8, 11}, {11, 12}, {12, 13}, {8, 14}, {14, 15}, {15, 16}};
-struct SparsePattern {
-    int n1[J], c1[J][J], o1[J];
-    int n2[J], c2[J][J], o2[J];
-    int nnz1, nnz2;
-};
-constexpr SparsePattern make_pattern() {
-    SparsePattern sp{};
-    bool a[J][J] = {};
-    for (int i = 0; i < J; ++i) a[i][i] = true;
-    for (int e = 0; e < 16; ++e) {
-        a[H36M_EDGES[e][0]][H36M_EDGES[e][1]] = true;
-        a[H36M_EDGES[e][1]][H36M_EDGES[e][0]] = true;
-    }
-    int t1 = 0, t2 = 0;
-    for (int i = 0; i < J; ++i) {
-        sp.n1[i] = 0;
-        sp.n2[i] = 0;
-        sp.o1[i] = t1;
-        sp.o2[i] = t2;
-        for (int j = 0; j < J; ++j) {
-            bool two = false;
-            for (int k = 0; k < J; ++k) two = two || (a[i][k] && a[k][j]);
-            if (a[i][j]) sp.c1[i][sp.n1[i]++] = j;
-            if (two) sp.c2[i][sp.n2[i]++] = j;
-        }
-        t1 += sp.n1[i];
-        t2 += sp.n2[i];
-    }
-    sp.nnz1 = t1;
-    sp.nnz2 = t2;
-    return sp;
-}
-constexpr SparsePattern SPAT = make_pattern();
-static_assert(SPAT.nnz1 == 49 && SPAT.nnz2 == 87, "H36M Chebyshev sparsity");
-
-// Chebyshev prologue: B2 = [T1 src | T2 src | src] (ChebConv.py:83, term order rotated so the
-// K=288 GEMM reads one buffer; the packed weights follow the same order).
-// Wave w = pose w, lane = column pair (lanes 48..63 idle), so a wave reads only rows its own
-// earlier LDS writes produced when it follows graph_mma (no workgroup barrier in between).
-// SPARSE: compile-time pattern, packed values (scalar loads); dense: 17x17 from the arena.
-// Sums run over increasing i in both (identical bits).
-// XSKIP (fp32 GEMM mode, Cheb1/Cheb2): write [- | T1 src | T2 src] and let the GEMM read the
-// T0 = src part from src itself (gemm_wave XS2), saving a third of the stores.
-template <bool SPARSE, int SPLIT = 0, bool XSKIP = false>
-__device__ __forceinline__ void cheb_prep(const float* __restrict__ cw, const float* src, float* b2, int wave,
-                                          int lane) {
-    lane = opaque(lane);
-    constexpr int G = 2, ng = D / G;
-    static_assert(ng <= 64 && P <= NW, "one pose per wave, one column pair per lane");
-    if (wave >= P || lane >= ng) return;
-    const int p = wave;
-    const int c = lane * G;
-    f32x2 v[J];
-#pragma unroll
-    for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
-    // T1 x = L x; T2 x = (2 L^2 - I) x by the Chebyshev recurrence 2 L (L x) - x (ChebConv.py:90-112
-    // builds T2 as a matrix first; the recurrence needs L's 49 nonzeros twice instead of T2's 87)
-    auto lx = [&](int j, const f32x2 (&u)[J]) {
-        f32x2 acc = {0.f, 0.f};
-        if constexpr (SPARSE) {
-#pragma unroll
-            for (int k = 0; k < SPAT.n1[j]; ++k) acc = pfma(splat2(cw[SPAT.o1[j] + k]), u[SPAT.c1[j][k]], acc);
-        } else {
-#pragma unroll
-            for (int i = 0; i < J; ++i) acc = pfma(splat2(cw[j * J + i]), u[i], acc);
-        }
-        return acc;
-    };
-    f32x2 t1[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) t1[j] = lx(j, v);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        const f32x2 t2 = pfma(splat2(2.0f), lx(j, t1), -v[j]);
-        if constexpr (SPLIT) {
-            char* row = reinterpret_cast<char*>(b2 + (p * J + j) * LD2);
-            split_store2<SPLIT>(row, c, t1[j]);
-            split_store2<SPLIT>(row, D + c, t2);
-            split_store2<SPLIT>(row, 2 * D + c, v[j]);
-        } else if constexpr (XSKIP) {
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t1[j];
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = t2;
-        } else {
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + c) = t1[j];
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + D + c) = t2;
-            *reinterpret_cast<f32x2*>(b2 + (p * J + j) * LD2 + 2 * D + c) = v[j];
-        }
-    }
-}
-
-// GraphNet products with the layer's dense 17x17 Laplacian L (GraFormer.py:174-183), L read
-// with uniform (scalar) loads.  One thread per (pose, column pair); in place.
-//   graph_apply:  buf[:, c] = L @ buf[:, c]
-//   graph_resid:  xs[:, c] += L @ y[:, c] + bias[c]   (fc2 reordered: L (X1 W2^T) + b2)
-// SPLIT_OUT (gemm mode 1, graph1): the product is fc1's A operand and is written split-fp16
-// into rows of stride LD2 (B2) instead of fp32 in place.
-template <bool RESID, int SPLIT_OUT = 0>
-__device__ __forceinline__ void graph_op(const float* __restrict__ L, const float* src, float* dst,
-                                         const float* __restrict__ bias, int tid) {
-    tid = opaque(tid);
-    constexpr int G = 2, ng = D / G;
-    if (tid >= P * ng) return;
-    const int p = tid / ng;
-    const int c = (tid - p * ng) * G;
-    f32x2 v[J];
-#pragma unroll
-    for (int i = 0; i < J; ++i) v[i] = *reinterpret_cast<const f32x2*>(src + (p * J + i) * LDX + c);
-    f32x2 bb = {0.f, 0.f};
-    if (RESID) bb = *reinterpret_cast<const f32x2*>(bias + c);
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        f32x2 acc = {0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < J; ++i) acc = pfma(splat2(L[j * J + i]), v[i], acc);
-        if constexpr (SPLIT_OUT) {
-            split_store2<SPLIT_OUT>(reinterpret_cast<char*>(dst + (p * J + j) * LD2), c, acc);
-            continue;
-        }
-        f32x2* o = reinterpret_cast<f32x2*>(dst + (p * J + j) * LDX + c);
-        if (RESID) {
-            *o = *o + (acc + bb);
-        } else {
-            *o = acc;
-        }
-    }
-}
-
-// GraphNet product on the matrix cores: wave w = pose w computes out^T = X^T L^T for its 17
-// rows with v_mfma_f32_16x16x4_f32 (M = 96 columns in 6 tiles, N = joints 0..15, K = joints in
-// 5 steps of 4, rows past 16 clamped and multiplied by zero), so lane l ends with out[j = l&15]
-// [c .. c+3] (16-byte stores).  Joint 16 (the 17th output row) from the same A fragments:
-// per-lane partial sums over the lane's k-slice, summed over the 4 lane groups by permlane.
-// LF: the layer's fragments (OFF_LGF): [s][lane] = L[lane&15][4s + (lane>>4)] and
-// [5 + s][lane] = L[16][4s + (lane>>4)] (0 past joint 16).
-//   RESID:     dst (stride LDX) += out + bias          (graph2: x + L (Y W2^T) + b2)
-//   SPLIT_OUT: out written split-fp16 into rows of stride LD2 (gemm mode 1, graph1)
-//   else:      dst (stride LDX) = out (in place allowed: each wave reads its rows before writing)
-// The fragments are loaded one phase ahead (gfrag_load) so their L2 latency hides there.
-// BIAS (graph2): also the lane's fc2 bias columns, so the RESID epilogue waits on no global load.
-struct GFrag {
-    float lb[5], l16[5];
-    f32x4 b4[6];
-    float b1[2];    // joint-16 row: bias of column cl of tiles g and 4 + (g & 1) (graph_mma's map)
-};
-template <bool BIAS = false>
-__device__ __forceinline__ GFrag gfrag_load(const float* __restrict__ LF, int lane,
-                                            const float* __restrict__ bias = nullptr) {
-    GFrag f;
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-        f.lb[s] = LF[s * 64 + lane];
-        f.l16[s] = LF[(5 + s) * 64 + lane];
-    }
-    if constexpr (BIAS) {
-        const int g = lane >> 4, cl = lane & 15;
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
-            f.b1[t] = bias[16 * t + cl];
-        }
-    }
-    return f;
-}
-// the bias part alone (issued a phase earlier than the fragments, see the kernel)
-__device__ __forceinline__ void gbias_load(GFrag& f, const float* __restrict__ bias, int lane) {
-    const int g = lane >> 4, cl = lane & 15;
-#pragma unroll
-    for (int t = 0; t < 6; ++t) f.b4[t] = *reinterpret_cast<const f32x4*>(bias + 16 * t + 4 * g);
-    f.b1[0] = bias[16 * g + cl];
-    f.b1[1] = bias[16 * (4 + (g & 1)) + cl];
-}
-
-// LNA: src is raw x; the operand is LayerNorm(x) formed in registers (fused LN1: statistics
-// from the O-proj epilogue in lst, gains/shifts ng/nb in LDS; see ln_row_norm).
-template <bool RESID, int SPLIT_OUT = 0, bool LNA = false>
-__device__ __forceinline__ void graph_mma(const GFrag& f, const float* src, float* dst,
-                                          const float* __restrict__ bias, int wave, int lane,
-                                          const float* lst = nullptr, const float* ng = nullptr,
-                                          const float* nb = nullptr) {
-    lane = opaque(lane);
-    if (wave >= P) return;
-    const int g = lane >> 4, cl = lane & 15;
-    const float(&lb)[5] = f.lb;
-    const float(&l16)[5] = f.l16;
-    const float* xp = src + wave * J * LDX + cl;
-    const int row_j = wave * J + cl, row16 = wave * J + 16;
-    // joint 16's output row: lane row g ends with column cl of tiles g and 4 + (g & 1)
-    // (reduce-scatter below); rows 2, 3 hold a duplicate of the second and store nothing
-    const int c16a = 16 * g + cl, c16b = 16 * (4 + (g & 1)) + cl;
-    // RESID: the residual rows this lane updates, read before the MFMAs (dst != src)
-    f32x4 old[6];
-    float old16a = 0.f, old16b = 0.f;
-    if constexpr (RESID) {
-#pragma unroll
-        for (int t = 0; t < 6; ++t) old[t] = *reinterpret_cast<const f32x4*>(dst + row_j * LDX + 16 * t + 4 * g);
-        old16a = dst[row16 * LDX + c16a];
-        old16b = dst[row16 * LDX + c16b];
-    }
-    float a[6][5];
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-        const int row = min(4 * s + g, J - 1);
-#pragma unroll
-        for (int t = 0; t < 6; ++t) a[t][s] = xp[row * LDX + 16 * t];
-    }
-    if constexpr (LNA) {
-        float gn[6], sh[6];
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            gn[t] = ng[16 * t + cl];
-            sh[t] = nb[16 * t + cl];
-        }
-#pragma unroll
-        for (int s = 0; s < 5; ++s) {
-            const f32x2 nrm = ln_row_norm(lst, wave * J + min(4 * s + g, J - 1));
-#pragma unroll
-            for (int t = 0; t < 6; ++t) a[t][s] = fmaf((a[t][s] - nrm[0]) * nrm[1], gn[t], sh[t]);
-        }
-    }
-    // k-steps outer, tiles inner: consecutive MFMAs are independent (no 5-deep dependent chain
-    // per tile); the first k-step starts from C = 0
-    f32x4 acc[6];
-    float p16[6];
-    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 5; ++s)
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], lb[s], s == 0 ? z : acc[t], 0, 0, 0);
-            p16[t] = s == 0 ? l16[0] * a[t][0] : fmaf(l16[s], a[t][s], p16[t]);
-        }
-#pragma unroll
-    for (int t = 0; t < 6; ++t) {
-        const int c0 = 16 * t + 4 * g;
-        if constexpr (SPLIT_OUT) {
-            split_store4<SPLIT_OUT>(reinterpret_cast<char*>(dst + row_j * LD2), c0, acc[t]);
-        } else if constexpr (RESID) {
-            *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = old[t] + (acc[t] + f.b4[t]);
-        } else {
-            *reinterpret_cast<f32x4*>(dst + row_j * LDX + c0) = acc[t];
-        }
-    }
-    // joint 16: the per-lane partial sums reduce-scattered over the 4 lane rows (rs4rows: lane
-    // row g gets register g's total; same summation order as sum4rows), 6 permlanes for 6 tiles
-    const float va = rs4rows(p16[0], p16[1], p16[2], p16[3]);    // tile g
-    const float vb = rs4rows(p16[4], p16[5], p16[4], p16[5]);    // tile 4 + (g & 1)
-    if constexpr (SPLIT_OUT) {
-        split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c16a, va);
-        if (g < 2) split_store1<SPLIT_OUT>(reinterpret_cast<char*>(dst + row16 * LD2), c16b, vb);
-    } else if constexpr (RESID) {
-        dst[row16 * LDX + c16a] = old16a + (va + f.b1[0]);
-        if (g < 2) dst[row16 * LDX + c16b] = old16b + (vb + f.b1[1]);
-    } else {
-        dst[row16 * LDX + c16a] = va;
-        if (g < 2) dst[row16 * LDX + c16b] = vb;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// gconv_input prologue: B1[:, 0:16] = [x | T1 x | T2 x | 0] for the 5 pose channels.
-template <bool SPARSE>
-__device__ __forceinline__ void input_prep(const float* __restrict__ cw, const float* xst, float* b1, int tid) {
-    tid = opaque(tid);
-    if (tid >= P * CIN) return;
-    const int p = tid / CIN, c = tid - p * CIN;
-    float v[J];
-#pragma unroll
-    for (int i = 0; i < J; ++i) v[i] = xst[(p * J + i) * CIN + c];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        float a1 = 0.f, a2 = 0.f;
-        if constexpr (SPARSE) {
-#pragma unroll
-            for (int k = 0; k < SPAT.n1[j]; ++k) a1 = fmaf(cw[SPAT.o1[j] + k], v[SPAT.c1[j][k]], a1);
-#pragma unroll
-            for (int k = 0; k < SPAT.n2[j]; ++k) a2 = fmaf(cw[SPAT.nnz1 + SPAT.o2[j] + k], v[SPAT.c2[j][k]], a2);
-        } else {
-#pragma unroll
-            for (int i = 0; i < J; ++i) {
-                a1 = fmaf(cw[j * J + i], v[i], a1);
-                a2 = fmaf(cw[J * J + j * J + i], v[i], a2);
-            }
-        }
-        float* rowp = b1 + (p * J + j) * LDX;
-        rowp[c] = v[j];
-        rowp[CIN + c] = a1;
-        rowp[2 * CIN + c] = a2;
-        if (c == 0) rowp[3 * CIN] = 0.f;
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// The sampler: K DDIM steps (or one eps evaluation, or one GCNpose forward) for P poses
-// per workgroup.
-template <int MODE, bool SPARSE, int G16>
-// `arena` is a separate restrict kernel argument: the compiler can then prove the weight arena
-// is never written during the launch and turns its wave-uniform loads (Laplacians, Chebyshev
-// terms, LayerNorm gains, biases) into scalar s_load (in the SampleArgs struct it cannot, and
-// every such value became a vector load with its L2 latency exposed).
-// G16: GEMMs on the split-fp16 path (gemm mode 1) with weights from `arena16`.
-__global__ void __launch_bounds__(NT, WG_PER_CU) sample_kernel(SampleArgs a, const float* __restrict__ arena,
-                                                               const char* __restrict__ arena16) {
-    constexpr bool EPS_MODE = MODE == M_EPS;
-    constexpr bool POSE = MODE == M_POSE;
-    __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
-    float* XS = sm + SM_XS;
-    float* B1 = sm + SM_B1;
-    float* B2 = sm + SM_B2;
-    float* XST = sm + SM_XST;
-    float* LNP = sm + SM_LNP;
-    float* ST = sm + SM_ST;
-    constexpr bool LNF = DPK_LN_FUSE && G16 == 0 && R == 68;   // fused LayerNorm (fp32 GEMM mode)
-    constexpr bool LN1F = LNF || (DPK_LN1_FUSE && G16 == 0 && R == 68);   // LN1 alone fused into graph1
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
-    const int pose0 = blockIdx.x * P;
-    const int npose = min(P, a.N - pose0);
-    const int nvalid = npose * PE;
-    const float* W = arena;
-    const float* CW = W + (SPARSE ? OFF_CHEBS : OFF_CHEB);
-
-    if constexpr (POSE) {
-        // uv into channels 0-1 of the 5-channel tile; the packed input weight is zero for 2-4
-        for (int i = tid; i < R * CIN; i += NT) {
-            const int row = i / CIN, c = i - row * CIN;
-            XST[i] = (c < CIN_POSE && row < npose * J) ? a.x_in[((size_t)pose0 * J + row) * CIN_POSE + c] : 0.f;
-        }
-    } else {
-        for (int i = tid; i < R * CIN; i += NT) XST[i] = i < nvalid ? a.x_in[(size_t)pose0 * PE + i] : 0.f;
-    }
-    // LayerNorm parameters of every layer, staged once per launch (the per-lane column slices
-    // are not wave-uniform, and as global loads their L2 latency sat on the LN critical path)
-    static_assert(OFF_LN0B == OFF_LN0A + D && OFF_LN1A == OFF_LN0A + 2 * D && OFF_LN1B == OFF_LN0A + 3 * D, "LN block");
-    for (int i = tid; i < NL * 4 * D; i += NT) LNP[i] = W[(i / (4 * D)) * LAYER_FLOATS + OFF_LN0A + i % (4 * D)];
-    for (int i = tid; i < 2 * J * J; i += NT) sm[SM_TC + i] = W[OFF_CHEB + i];
-    if (WG_PER_CU == 2 && a.phase_delay > 0 && blockIdx.x >= (gridDim.x + 1) / 2) {
-        // de-phase the two co-resident workgroups of a CU so one runs its VALU phases while the
-        // other runs MFMA phases (the dispatcher fills second CU slots with the grid's second half)
-        const long long t0 = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t0 < a.phase_delay) __builtin_amdgcn_s_sleep(8);
-    }
-    __syncthreads();
-
-    const int K = MODE == M_SAMPLE ? a.K : 1;
-#if DPK_TRACE
-    if ((tid & 63) == 0) {
-        tr_row[wave] = nullptr;
-        tr_ix[wave] = 0;
-    }
-#define DPK_STAMP()                                                                                       \
-    do {                                                                                                  \
-        if ((tid & 63) == 0)                                                                              \
-            tr_row[wave] = (a.trace && s == a.trace_step)                                                 \
-                               ? a.trace + ((size_t)blockIdx.x * NW + wave) * TRACE_SLOTS                 \
-                               : nullptr;                                                                 \
-        tr_stamp();                                                                                       \
-    } while (0)
-#define BAR()          \
-    do {               \
-        DPK_STAMP();   \
-        __syncthreads(); \
-        DPK_STAMP();   \
-    } while (0)
-#else
-#define BAR() __syncthreads()
-#endif
-#pragma unroll 1
-    for (int s = 0; s < K; ++s) {
-        // LNF: QKV's first B k-blocks are in flight a whole GEMM ahead (the LN phase that used to
-        // cover their L2 latency is gone): layer 0's here, layer l+1's before layer l's Cheb2 GEMM
-        BPre<9> qpre;
-        if constexpr (LNF) qpre = gemm_prefetch<18, 6>(W + OFF_QKV, wave, lane);
-        // ---- gconv_input: ChebConv 5->96 (gcndiff.py:108)
-        {
-            const auto pre = gemm_prefetch<6, 1>(W + OFF_WIN, wave, lane);
-            input_prep<SPARSE>(CW, XST, B1, tid);
-            BAR();
-            const EpiArgs e{XS, LDX, W + OFF_BIN, nullptr, 0, pose0, a.N - 1, ST};
-            gemm_wg<6, 1, E_STORE, LNF>(B1, LDX, W + OFF_WIN, wave, lane, e, pre);
-        }
-        BAR();
-
-#pragma unroll 1
-        for (int l = 0; l < a.num_layers; ++l) {
-            const float* LW = W + l * LAYER_FLOATS;
-            const char* L16 = arena16 + (size_t)l * LAYER16_BYTES;
-            char* B1b = reinterpret_cast<char*>(B1);
-            char* B2b = reinterpret_cast<char*>(B2);
-            // ---- x = x + MHA(LN0(x))   (GraAttenLayer, GraFormer.py:94-95)
-            {
-                const EpiArgs e{B2, LD2, LW + OFF_BQKV, nullptr, 0, pose0, a.N - 1};
-                if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<G16, 18, KB32_D>(L16 + O16_QKV, wave, lane);
-                    if (DPK_RUN(8)) layer_norm<G16>(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
-                    BAR();
-                    if (DPK_RUN(16 | 32)) gemm_wg16<G16, 18, KB32_D, E_STORE, 0>(B1b, LDX * 4, L16 + O16_QKV, wave, lane, e, pre);
-                } else if constexpr (LNF) {
-                    // LN0 fused: QKV reads x and normalises its A operand (partials from Cheb2 / gconv_input)
-                    if (DPK_RUN(16 | 32))
-                        gemm_wg<18, 6, E_STORE, false, true>(XS, LDX, LW + OFF_QKV, wave, lane, e, qpre, ST,
-                                                             LNP + l * 4 * D, LNP + l * 4 * D + D);
-                } else {
-                    const auto pre = gemm_prefetch<18, 6>(LW + OFF_QKV, wave, lane);
-                    if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D, LNP + l * 4 * D + D, tid);
-                    BAR();
-                    if (DPK_RUN(16 | 32)) gemm_wg<18, 6, E_STORE>(B1, LDX, LW + OFF_QKV, wave, lane, e, pre);
-                }
-            }
-            BAR();
-            {
-                const EpiArgs e{XS, LDX, LW + OFF_BO, nullptr, 0, pose0, a.N - 1, ST};
-                if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<G16, 6, KB32_D>(L16 + O16_O, wave, lane);
-                    if (DPK_RUN(1)) {
-                        if constexpr (DPK_ATTN_MMA) attention_mma<G16>(B2, B1, a.mask, wave, lane);
-                        else attention<G16>(B2, B1, a.mask, tid);
-                    }
-                    BAR();
-                    if (DPK_RUN(16 | 64)) gemm_wg16<G16, 6, KB32_D, E_RESID, 0>(B1b, LDX * 4, L16 + O16_O, wave, lane, e, pre);
-                } else {
-                    const auto pre = gemm_prefetch<6, 6>(LW + OFF_O, wave, lane);
-                    if (DPK_RUN(1)) {
-                        if constexpr (DPK_ATTN_MMA) attention_mma(B2, B1, a.mask, wave, lane);
-                        else attention(B2, B1, a.mask, tid);
-                    }
-                    BAR();
-                    if (DPK_RUN(16 | 64)) gemm_wg<6, 6, E_RESID, LN1F>(B1, LDX, LW + OFF_O, wave, lane, e, pre);
-                }
-            }
-            BAR();
-            // ---- x = x + GraphNet(LN1(x)) = x + L (relu((L LN1(x)) W1^T + b1) W2^T) + b2
-            //      (GraFormer.py:189-201; fc2's product with L applied after the GEMM)
-            //      split path: graph1 writes fc1's A operand split into B2[:, 0:96]; fc1 writes
-            //      fc2's split A operand into B2[:, 96:288] (bytes 384..1152 of the row)
-            GFrag gb;   // graph2's fc2 bias: issued here, beside fc1's first B blocks
-            gbias_load(gb, LW + OFF_BFC2, lane);
-            if constexpr (G16) {
-                const auto pre = gemm16_prefetch<G16, 12, KB32_D>(L16 + O16_FC1, wave, lane);
-                const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
-                if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
-                BAR();
-                if (DPK_RUN(2)) graph_mma<false, G16>(gf, B1, B2, nullptr, wave, lane);
-                BAR();
-                if (DPK_RUN(16 | 128)) {
-                    const EpiArgs e{B2 + D, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg16<G16, 12, KB32_D, E_STORE_RELU, G16>(B2b, LD2 * 4, L16 + O16_FC1, wave, lane, e, pre);
-                }
-            } else {
-                const auto pre = gemm_prefetch<12, 6>(LW + OFF_FC1, wave, lane);
-                const GFrag gf = gfrag_load(LW + OFF_LGF, lane);
-                if constexpr (LN1F) {
-                    // LN1 fused into the GraphNet product's operand (partials from the O-proj epilogue)
-                    if (DPK_RUN(2))
-                        graph_mma<false, 0, true>(gf, XS, B1, nullptr, wave, lane, ST, LNP + l * 4 * D + 2 * D,
-                                                  LNP + l * 4 * D + 3 * D);
-                } else {
-                    if (DPK_RUN(8)) layer_norm(XS, B1, LNP + l * 4 * D + 2 * D, LNP + l * 4 * D + 3 * D, tid);
-                    BAR();
-                    if (DPK_RUN(2)) graph_mma<false>(gf, B1, B1, nullptr, wave, lane);
-                }
-                BAR();
-                if (DPK_RUN(16 | 128)) {
-                    const EpiArgs e{B2, LD2, LW + OFF_BFC1, nullptr, 0, pose0, a.N - 1};
-                    gemm_wg<12, 6, E_STORE_RELU>(B1, LDX, LW + OFF_FC1, wave, lane, e, pre);
-                }
-            }
-            GFrag gf2 = gfrag_load(LW + OFF_LGF, lane);   // graph2's operands, a GEMM ahead
-#pragma unroll
-            for (int t = 0; t < 6; ++t) {
-                gf2.b4[t] = gb.b4[t];
-                gf2.b1[t] = gb.b1[t];
-            }
-            {
-                const EpiArgs e{B1, LDX, nullptr, nullptr, 0, pose0, a.N - 1};
-                if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<G16, 6, KB32_D2>(L16 + O16_FC2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(16 | 256))
-                        gemm_wg16<G16, 6, KB32_D2, E_STORE_NB, 0>(B2b + D * 4, LD2 * 4, L16 + O16_FC2, wave, lane, e, pre);
-                } else {
-                    const auto pre = gemm_prefetch<6, 12>(LW + OFF_FC2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(16 | 256)) gemm_wg<6, 12, E_STORE_NB>(B2, LD2, LW + OFF_FC2, wave, lane, e, pre);
-                }
-            }
-            {
-                const float* tp = a.tproj + (MODE == M_SAMPLE ? (size_t)s * NL * D : 0) + l * D;
-                const EpiArgs e{B1, LDX, LW + OFF_BC1, tp, EPS_MODE ? NL * D : 0, pose0, a.N - 1};
-                if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<G16, 6, KB32_D3>(L16 + O16_C1, wave, lane);
-                    BAR();
-                    if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
-                    // ---- _ResChebGC_diff (gcndiff.py:47-53): x + relu(Cheb2(relu(Cheb1(x)) + temb_proj));
-                    //      cheb_prep reads only its own wave's rows of XS (wave = pose): no barrier
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, G16>(CW, XS, B2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(16 | 512)) gemm_wg16<G16, 6, KB32_D3, E_CHEB1, 0>(B2b, LD2 * 4, L16 + O16_C1, wave, lane, e, pre);
-                } else {
-                    const auto pre = gemm_prefetch<6, 18>(LW + OFF_C1, wave, lane);
-                    BAR();
-                    if (DPK_RUN(2)) graph_mma<true>(gf2, B1, XS, LW + OFF_BFC2, wave, lane);
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, 0, true>(CW, XS, B2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(16 | 512))
-                        gemm_wg<6, 18, E_CHEB1, false, false, true>(B2, LD2, LW + OFF_C1, wave, lane, e, pre, nullptr,
-                                                                    nullptr, nullptr, XS, LDX);
-                }
-            }
-            {
-                const EpiArgs e{XS, LDX, LW + OFF_BC2, nullptr, 0, pose0, a.N - 1, ST};
-                if constexpr (G16) {
-                    const auto pre = gemm16_prefetch<G16, 6, KB32_D3>(L16 + O16_C2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, G16>(CW, B1, B2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(16 | 1024))
-                        gemm_wg16<G16, 6, KB32_D3, E_RESID_RELU, 0>(B2b, LD2 * 4, L16 + O16_C2, wave, lane, e, pre);
-                } else {
-                    const auto pre = gemm_prefetch<6, 18>(LW + OFF_C2, wave, lane);
-                    BAR();
-                    if (DPK_RUN(4)) cheb_prep<SPARSE, 0, true>(CW, B1, B2, wave, lane);
-                    BAR();
-                    if constexpr (LNF)
-                        if (l + 1 < a.num_layers) qpre = gemm_prefetch<18, 6>(LW + LAYER_FLOATS + OFF_QKV, wave, lane);
-                    if (DPK_RUN(16 | 1024))
-                        gemm_wg<6, 18, E_RESID_RELU, LNF, false, true>(B2, LD2, LW + OFF_C2, wave, lane, e, pre,
-                                                                       ST, nullptr, nullptr, B1, LDX);
-                }
-            }
-            BAR();
-        }
-        // ---- gconv_output: ChebConv 96->5 (gcndiff.py:112), then the DDIM update
-        //      (pose: ChebConv 96->3, gcnpose.py:112, kept in B1 for the uvxyz assembly).
-        //      sum_k T_k x W_k computed as sum_k T_k (x W_k): one K=96 GEMM Y = x [W0 | W1 | W2]
-        //      (3*cout columns, one tile) into B2, then the 17x17 products on the 3*cout columns.
-        constexpr int COUTK = POSE ? COUT_POSE : COUT;
-        constexpr int NOUT = P * J * COUTK, NIT = (NOUT + NT - 1) / NT;
-        const auto preo = out_prefetch<KB_D>(W + OFF_WOUT, lane);
-        float bo[NIT];                                  // output bias of this thread's outputs, a GEMM ahead
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) bo[k] = W[OFF_BOUT + (tid + k * NT) % COUTK];
-        if (wave < R / 16)
-            gemm_out<KB_D, 3 * COUTK>(XS, LDX, W + OFF_WOUT, wave, lane,
-                                      [&](int r, int c, float v) { B2[r * LD2 + c] = v; }, preo);
-        BAR();
-        {
-            float cf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-            if constexpr (MODE == M_SAMPLE) {
-                const float* cfp = a.coef + s * 6;
-#pragma unroll
-                for (int i = 0; i < 5; ++i) cf[i] = cfp[i];                  // uniform: SGPRs
-            }
-            const float* T1d = sm + SM_TC;
-            const float* T2d = T1d + J * J;
-#pragma unroll
-            for (int k = 0; k < NIT; ++k) {
-                const int idx = tid + k * NT;
-                if (idx >= NOUT) break;
-                const int p = idx / (J * COUTK), rem = idx - p * (J * COUTK);
-                const int j = rem / COUTK, c = rem - j * COUTK;
-                const float* yp = B2 + p * J * LD2;
-                float a1 = 0.f, a2 = 0.f;
-#pragma unroll
-                for (int i = 0; i < J; ++i) {
-                    a1 = fmaf(T1d[j * J + i], yp[i * LD2 + COUTK + c], a1);
-                    a2 = fmaf(T2d[j * J + i], yp[i * LD2 + 2 * COUTK + c], a2);
-                }
-                const float et = ((yp[j * LD2 + c] + a1) + a2) + bo[k];
-                const int r = p * J + j;
-                const int oidx = r * CIN + c;          // same as r*COUT+c (coords 5 -> 5)
-                const bool valid = oidx < nvalid;
-                const size_t gidx = (size_t)pose0 * PE + oidx;
-                if (POSE) {
-                    B1[r * LDX + c] = et;
-                } else if (EPS_MODE) {
-                    if (valid) a.x_out[gidx] = et;
-                } else {
-                    const float z = a.eta != 0.f ? normal_noise(a.seed, s, (long long)gidx) : 0.f;
-                    float x0, xn;
-                    ddim_elem(cf, XST[oidx], et, z, x0, xn);
-                    XST[oidx] = xn;
-                    if (valid) {
-                        if (a.x0s) a.x0s[(size_t)s * a.N * PE + gidx] = x0;
-                        if (a.xs) a.xs[(size_t)(s + 1) * a.N * PE + gidx] = xn;
-                    }
-                }
-            }
-        }
-        BAR();
-    }
-    if constexpr (MODE == M_SAMPLE) {
-        for (int i = tid; i < nvalid; i += NT) a.x_out[(size_t)pose0 * PE + i] = XST[i];
-    } else if constexpr (POSE) {
-        // inputs_xyz = model_pose(input_2d); inputs_xyz -= root; input_uvxyz = cat(uv, xyz).repeat(H)
-        // (runners/diffpose_frame.py:337-342).  root_mode 0 = what the reference's aliased in-place
-        // `x[:, :, :] -= x[:, :1, :]` yields on CPU torch (only the root row is zeroed).
-        if (a.x_out)
-            for (int i = tid; i < npose * J * COUT_POSE; i += NT) {
-                const int row = i / COUT_POSE, c = i - row * COUT_POSE;
-                a.x_out[(size_t)pose0 * J * COUT_POSE + i] = B1[row * LDX + c];
-            }
-        if (a.uvxyz)
-            for (int i = tid; i < npose * PE; i += NT) {
-                const int row = i / CIN, c = i - row * CIN;
-                float v;
-                if (c < CIN_POSE) {
-                    v = XST[i];
-                } else {
-                    const float raw = B1[row * LDX + (c - CIN_POSE)];
-                    const int j = row % J;
-                    if (a.root_mode == 0) v = j == 0 ? 0.f : raw;
-                    else if (a.root_mode == 1) v = raw - B1[(row - j) * LDX + (c - CIN_POSE)];
-                    else v = raw;
-                }
-                for (int hh = 0; hh < a.H; ++hh) a.uvxyz[((size_t)hh * a.N + pose0) * PE + i] = v;
-            }
-    }
-}
-
-#undef BAR
-#undef DPK_STAMP
+namespace dpk {
 
 // ---------------------------------------------------------------------------------------
 // Timestep MLP (gcndiff.py:15-33, :103-106) and per-layer temb_proj(swish(.)) (:46, :51):
@@ -2378,7 +200,8 @@ struct dpk_handle {
     int device = 0;
     int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
-    int phase_delay = 0;           // DPK_PHASE_DELAY (cycles), two-workgroups-per-CU builds only
+    int n_cu = 256;                // compute units of the device (workgroups per round)
+    bool tail_split = true;        // balance the last round with 2-pose tiles (launch_sampler)
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
@@ -2608,19 +431,54 @@ static int upload(dpk_handle* h) {
     return DPK_OK;
 }
 
-// the sampler kernel for the handle's graph pattern and GEMM mode
-template <int MODE>
-static void launch_sampler(dpk_handle* h, dim3 grid, hipStream_t st, const SampleArgs& a) {
+// One launch of the sampler kernel with tile size PT (4: dpk, 2: dpk2) for the handle's graph
+// pattern and GEMM mode.
+template <int MODE, int PT>
+static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st, const SampleArgs& a) {
     const int gm = h->gemm_mode;
     const char* a16 = gm == 2 ? h->arenabf : h->arena16;
-    if (h->sparse_graph) {
-        if (gm == 1) hipLaunchKernelGGL((sample_kernel<MODE, true, 1>), grid, dim3(NT), 0, st, a, h->arena, a16);
-        else if (gm == 2) hipLaunchKernelGGL((sample_kernel<MODE, true, 2>), grid, dim3(NT), 0, st, a, h->arena, a16);
-        else hipLaunchKernelGGL((sample_kernel<MODE, true, 0>), grid, dim3(NT), 0, st, a, h->arena, a16);
-    } else {
-        if (gm == 1) hipLaunchKernelGGL((sample_kernel<MODE, false, 1>), grid, dim3(NT), 0, st, a, h->arena, a16);
-        else if (gm == 2) hipLaunchKernelGGL((sample_kernel<MODE, false, 2>), grid, dim3(NT), 0, st, a, h->arena, a16);
-        else hipLaunchKernelGGL((sample_kernel<MODE, false, 0>), grid, dim3(NT), 0, st, a, h->arena, a16);
+    const dim3 grid(blocks), block(NT);
+#define DPK_LAUNCH(NS)                                                                                          \
+    do {                                                                                                        \
+        if (h->sparse_graph) {                                                                                  \
+            if (gm == 1) hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 1>), grid, block, shmem, st, a, h->arena, a16);  \
+            else if (gm == 2) hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 2>), grid, block, shmem, st, a, h->arena, a16); \
+            else hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 0>), grid, block, shmem, st, a, h->arena, a16);          \
+        } else {                                                                                                \
+            if (gm == 1) hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 1>), grid, block, shmem, st, a, h->arena, a16); \
+            else if (gm == 2) hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 2>), grid, block, shmem, st, a, h->arena, a16); \
+            else hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 0>), grid, block, shmem, st, a, h->arena, a16);         \
+        }                                                                                                       \
+    } while (0)
+    if constexpr (PT == 4) DPK_LAUNCH(dpk);
+    else DPK_LAUNCH(dpk2);
+#undef DPK_LAUNCH
+}
+
+// The sampler over a.N poses.  One 4-pose workgroup per CU per round; when the last round would
+// leave at least half the CUs idle (at most 2 poses per CU remain) those poses run instead as
+// 2-pose workgroups (dpk2, about 0.6 of a 4-pose tile's time), one per CU, in a second launch
+// after the full rounds.  E.g. config 5's 2,560 poses per GPU: 2 full rounds + 256 2-pose tiles
+// instead of 2.5 rounds of 4-pose tiles (3 round times).  Each workgroup's result depends only on
+// its own poses, so the split changes no bits.
+template <int MODE>
+static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a) {
+    const int N = a.N;
+    const int round4 = P * h->n_cu;
+    int n4 = N;
+    const int rem = N % round4;
+    if (h->tail_split && rem != 0 && rem <= 2 * h->n_cu) n4 = N - rem;
+    if (n4 > 0) {
+        a.pose_off = 0;
+        launch_tiles<MODE, P>(h, (n4 + P - 1) / P, 0, st, a);
+    }
+    if (n4 < N) {
+        // pad the 2-pose kernel's LDS past half a CU's so the dispatcher places one per CU
+        constexpr int P2 = dpk2::P;
+        constexpr size_t half = 160 * 1024 / 2, lds2 = (size_t)dpk2::SM_FLOATS * 4;
+        constexpr size_t pad = lds2 > half ? 0 : half - lds2 + 256;
+        a.pose_off = n4;
+        launch_tiles<MODE, P2>(h, (N - n4 + P2 - 1) / P2, pad, st, a);
     }
 }
 
@@ -2651,12 +509,15 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     h->kind = kind;
     h->num_layers = cfg->num_layers;
     if (hipSetDevice(h->device) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) {
         delete h;
         return DPK_E_HIP;
     }
-    if (const char* pd = getenv("DPK_PHASE_DELAY")) h->phase_delay = atoi(pd);
-    else h->phase_delay = WG_PER_CU == 2 ? 60000 : 0;
+    h->n_cu = std::max(h->n_cu, 1);
+    // DPK_TAIL_SPLIT=0: every round in 4-pose tiles (A/B timing); trace builds stamp per block id
+    if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_split = atoi(ts) != 0;
+    if (DPK_TRACE) h->tail_split = false;
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_arena16.assign(ARENA16_BYTES / 2, 0);
     h->h_arenabf.assign(ARENA16_BYTES / 2, 0);
@@ -3021,7 +882,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
-    launch_sampler<M_EPS>(h, dim3((N + P - 1) / P), st, a);
+    launch_sampler<M_EPS>(h, st, a);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -3057,7 +918,6 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.mask = h->mask;
     a.eta = sc->eta;
     a.seed = seed;
-    a.phase_delay = h->phase_delay;
     a.num_layers = h->num_layers;
 #if DPK_TRACE
     if (h->trace_step >= 0) {
@@ -3075,7 +935,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    launch_sampler<M_SAMPLE>(h, dim3((N + P - 1) / P), st, a);
+    launch_sampler<M_SAMPLE>(h, st, a);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return sched_note_use(h, sc, st, cap);
@@ -3109,7 +969,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
-    launch_sampler<M_POSE>(h, dim3((N + P - 1) / P), st, a);
+    launch_sampler<M_POSE>(h, st, a);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;

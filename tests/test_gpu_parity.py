@@ -149,6 +149,40 @@ def test_large_batch_property(model, mask):
     assert torch.equal(big.view(20, 1024, 17, 5), base.unsqueeze(0).expand(20, -1, -1, -1))
 
 
+def test_tail_round_in_two_pose_tiles(model, mask):
+    """Config 5's per-GPU share (2,560 poses = 2.5 rounds of 4-pose workgroups on 256 CUs) runs as
+    2 full rounds of 4-pose tiles plus one round of 2-pose tiles (launch_sampler).  Each part is
+    bitwise the same as running its poses alone (the 2,048-pose head is 2 full rounds; the 512-pose
+    tail alone is one round of 2-pose tiles), the tail is within the fp32 bars of the oracle, and
+    a handle with the split disabled (DPK_TAIL_SPLIT=0: the tail as a half round of 4-pose tiles)
+    agrees within rounding (the tiles put different joints on the 4-row tail path)."""
+    import os
+    from oracle import gcndiff_oracle as O
+
+    x, _ = synthetic_batch(2560, seed=23)
+    xt = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, 10)
+    out = model.sample(xt, seq, _betas(51), mask=mask)
+    head = model.sample(xt[:2048].contiguous(), seq, _betas(51), mask=mask)
+    tail = model.sample(xt[2048:].contiguous(), seq, _betas(51), mask=mask)
+    assert torch.equal(out[:2048], head) and torch.equal(out[2048:], tail)
+    os.environ["DPK_TAIL_SPLIT"] = "0"
+    try:
+        m4 = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+    finally:
+        del os.environ["DPK_TAIL_SPLIT"]
+    m4.load_state_dict(synthetic_state_dict())
+    out4 = m4.sample(xt, seq, _betas(51), mask=mask)
+    m4.close()
+    assert torch.equal(out4[:2048], head)
+    assert _maxdiff(out4, out) <= TRAJ_TOL
+    P, adj = O.params_to_torch(synthetic_state_dict()), O.adjacency()
+    sel = torch.tensor([2048, 2049, 2050, 2051, 2558, 2559])
+    xs, _ = O.generalized_steps(torch.from_numpy(x)[sel], torch.ones(1, 1, 17, dtype=torch.bool), seq,
+                                lambda a_, m_, t_: O.gcndiff_forward(P, adj, a_, m_, t_), _betas(51))
+    assert _maxdiff(out[sel.cuda()], xs[-1]) <= TRAJ_TOL
+
+
 def test_eta_noise_statistics(model, mask):
     """eta > 0 draws N(0,1) noise in-kernel (counter-based; not torch.randn_like): check
     determinism per seed and the moments of the recovered noise (parity is statistical)."""
