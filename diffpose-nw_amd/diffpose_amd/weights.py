@@ -182,3 +182,75 @@ def load_checkpoint(path: str, kind: str = "diff", n_layers: int = N_LAYERS) -> 
     if isinstance(states, (list, tuple)):
         states = states[0]
     return normalize_state_dict(states, kind=kind, n_layers=n_layers)
+
+
+def reference_init_state_dict(seed: int, n_layers: int = N_LAYERS, hid: int = HID, n_pts: int = N_PTS,
+                              coords=COORDS) -> "OrderedDict[str, np.ndarray]":
+    """GCNdiff's weights exactly as the reference constructor draws them after
+    ``torch.manual_seed(seed)`` (float32 numpy, no prefix) — the initialisers a freshly built
+    reference model carries, for parity on the reference's own value range.
+
+    Restates the parameter-drawing order of ``GCNdiff.__init__`` (models/gcndiff.py:55-99) with
+    torch's own initialisers, consuming torch's global generator in the same sequence:
+      1. gconv_input ``ChebConv(5, 96, K=2)``: xavier_normal_ on the (3,1,in,out) weight, zero
+         bias (models/ChebConv.py:59-67);
+      2. one ``nn.Linear(96, 96)`` deep-copied into the 4 attention projections
+         (``clones``, models/GraFormer.py:55, :123) and ``copy.deepcopy``'d into every layer
+         (models/gcndiff.py:80-89): all 4 projections of all layers start equal;
+      3. one ``GraphNet(96, 96, 17)``: A_hat = I, fc 96->192 then 192->96 (GraFormer.py:191-196),
+         likewise copied into every layer;
+      4. per layer: Cheb 96->96 (gconv1), Cheb 96->96 (gconv2), temb_proj Linear(384, 96)
+         (models/gcndiff.py:39-46); LayerNorm gains 1, shifts 0 (GraFormer.py:63-64);
+      5. gconv_output ``ChebConv(96, 5, K=2)``; 6. temb.dense Linear(96, 384), Linear(384, 384).
+    Pinned by the sha256 the golden generator takes of the reference model built under the same
+    seed (tests/golden/meta.json "refinit_sha256")."""
+    import torch
+    from torch import nn
+
+    emb = 4 * hid
+    state = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(seed)
+
+        def cheb(cin, cout):
+            w = torch.empty(3, 1, cin, cout)
+            nn.init.xavier_normal_(w)
+            return w, torch.zeros(1, 1, cout)
+
+        def linear(cin, cout):
+            m = nn.Linear(cin, cout)
+            return m.weight.detach().clone(), m.bias.detach().clone()
+
+        win, bin_ = cheb(coords[0], hid)
+        attn = linear(hid, hid)
+        fc1 = linear(hid, 2 * hid)
+        fc2 = linear(2 * hid, hid)
+        layers = []
+        for _ in range(n_layers):
+            layers.append((cheb(hid, hid), cheb(hid, hid), linear(emb, hid)))
+        wout, bout = cheb(hid, coords[1])
+        d0 = linear(hid, emb)
+        d1 = linear(emb, emb)
+    finally:
+        torch.random.set_rng_state(state)
+    sd = {"gconv_input.weight": win, "gconv_input.bias": bin_}
+    for i, (g1, g2, tp) in enumerate(layers):
+        p = f"gconv_layers.{i}."
+        sd[p + "gconv1.gconv.weight"], sd[p + "gconv1.gconv.bias"] = g1
+        sd[p + "gconv2.gconv.weight"], sd[p + "gconv2.gconv.bias"] = g2
+        sd[p + "temb_proj.weight"], sd[p + "temb_proj.bias"] = tp
+    for i in range(n_layers):
+        p = f"atten_layers.{i}."
+        for j in range(4):
+            sd[p + f"self_attn.linears.{j}.weight"], sd[p + f"self_attn.linears.{j}.bias"] = attn
+        sd[p + "feed_forward.A_hat"] = torch.eye(n_pts)
+        sd[p + "feed_forward.gconv1.fc.weight"], sd[p + "feed_forward.gconv1.fc.bias"] = fc1
+        sd[p + "feed_forward.gconv2.fc.weight"], sd[p + "feed_forward.gconv2.fc.bias"] = fc2
+        for j in range(2):
+            sd[p + f"sublayer.{j}.norm.a_2"] = torch.ones(hid)
+            sd[p + f"sublayer.{j}.norm.b_2"] = torch.zeros(hid)
+    sd["gconv_output.weight"], sd["gconv_output.bias"] = wout, bout
+    sd["temb.dense.0.weight"], sd["temb.dense.0.bias"] = d0
+    sd["temb.dense.1.weight"], sd["temb.dense.1.bias"] = d1
+    shapes = param_shapes(hid=hid, n_layers=n_layers, n_pts=n_pts, coords=coords)
+    return OrderedDict((k, np.ascontiguousarray(sd[k].numpy(), dtype=np.float32)) for k in shapes)

@@ -221,3 +221,34 @@ def test_load_checkpoint_reference_format(tmp_path):
     torch.save([{"module." + k: torch.from_numpy(v.copy()) for k, v in psd.items()}], str(path))
     gp = load_checkpoint(str(path), kind="pose")
     assert all(np.array_equal(gp[k], psd[k]) for k in psd)
+
+
+# ---- other weight distributions (golden groups g9/g10) ----------------------------------------
+def _weights_for(name):
+    from diffpose_amd.weights import reference_init_state_dict
+
+    if name.startswith("g9_refinit_seed"):
+        return reference_init_state_dict(int(name[len("g9_refinit_seed"):].split(".")[0]))
+    return synthetic_state_dict(seed=7)
+
+
+def test_reference_initialisers_restated_exactly():
+    """weights.reference_init_state_dict(s) == the state_dict of the reference GCNdiff built under
+    torch.manual_seed(s) (sha256 taken by tools/gen_goldens.py from the reference model itself)."""
+    from diffpose_amd.weights import reference_init_state_dict
+
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    for s, sha in meta["refinit_sha256"].items():
+        assert state_dict_sha256(reference_init_state_dict(int(s))) == sha
+    assert state_dict_sha256(synthetic_state_dict(seed=7)) == meta["seed7_weights_sha256"]
+
+
+@pytest.mark.parametrize("name", ["g9_refinit_seed0.npz", "g9_refinit_seed1.npz", "g10_synth_seed7.npz"])
+def test_oracle_on_other_weights(golden, graph, name):
+    g = golden(name)
+    P = O.params_to_torch(_weights_for(name))
+    mask = torch.ones(1, 1, 17, dtype=torch.bool)
+    _close(O.gcndiff_forward(P, graph, torch.from_numpy(g["x"][:8]), mask, torch.from_numpy(g["t8"])).numpy(), g["eps"])
+    fn = lambda xt, m, tt: O.gcndiff_forward(P, graph, xt, m, tt)  # noqa: E731
+    xs, _ = O.generalized_steps(torch.from_numpy(g["x"]), mask, [int(s) for s in g["seq"]], fn, _betas(int(g["T"])))
+    _close(xs[-1].numpy(), g["out"])

@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
-    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g8); default all")
+    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g9); default all")
     args = ap.parse_args()
     only = set(x for x in args.only.split(",") if x)
 
@@ -253,6 +253,62 @@ def main():
                  uvxyz=np.stack([it[0].numpy() for it in items]), noise_scale=np.stack([it[1].numpy() for it in items]),
                  pose_2d=np.stack([it[2].numpy() for it in items]), pose_3d=np.stack([it[3].numpy() for it in items]),
                  actions=np.array([it[4] for it in items]), camerapara=np.stack([it[5].numpy() for it in items]))
+
+    # ---------------- G9/G10: other weight distributions ----------------
+    # G9: the reference's OWN initialisers (a freshly constructed GCNdiff under torch.manual_seed(s),
+    # models/ChebConv.py:62-67, models/gcndiff.py:70-98), s = 0, 1; G10: the build's generator at a
+    # second seed (7).  Each: eps at mixed t, and the K=50 final in fp32 and in fp64 (the model and
+    # schedule cast to double; the timestep embedding and the Chebyshev tables are float32 by
+    # construction, so they are cast for that run) — the fp32-vs-fp64 gap sets the tolerance scale for these weights.
+    if want("g9"):
+        import models.gcndiff as gcndiff_mod
+        from diffpose_amd.weights import reference_init_state_dict
+
+        def fixture(m, name, seed_x, extra):
+            xq, tgt = synthetic_batch(32, seed=seed_x)
+            xq = torch.from_numpy(xq)
+            t8 = torch.tensor([49.0, 0.0, 12.0, 31.0, 7.0, 49.0, 25.0, 3.0])
+            b = torch.from_numpy(get_beta_schedule("linear", beta_start=0.0001, beta_end=0.001,
+                                                   num_diffusion_timesteps=51)).float()
+            seq50 = list(range(0, 50, 1))
+            with torch.no_grad():
+                eps = m(xq[:8], mask, t8, 0)
+            xs, _ = generalized_steps(xq, mask, seq50, m, b, eta=0.0)
+            m64 = copy.deepcopy(m).double()
+            m64.adj = adj.double()
+            for layer in m64.gconv_layers:
+                layer.adj = m64.adj
+            # float32 by construction in the reference: the timestep embedding and the Chebyshev
+            # tables (models/ChebConv.py:98-99); cast to double for this run only
+            orig = gcndiff_mod.get_timestep_embedding
+            orig_cp = ChebConv.cheb_polynomial
+            gcndiff_mod.get_timestep_embedding = lambda t, d: orig(t, d).double()
+            ChebConv.cheb_polynomial = lambda self_, L: orig_cp(self_, L.float()).to(L.dtype)
+            try:
+                xs64, _ = generalized_steps(xq.double(), mask, seq50, m64, b.double(), eta=0.0)
+            finally:
+                gcndiff_mod.get_timestep_embedding = orig
+                ChebConv.cheb_polynomial = orig_cp
+            np.savez(os.path.join(args.out, name), x=xq.numpy(), t8=t8.numpy(), eps=eps.numpy(), seq=np.array(seq50),
+                     T=51, out=xs[-1].numpy(), out64=xs64[-1].numpy(), targets=tgt, **extra)
+
+        import copy
+        shas = {}
+        for s_ in (0, 1):
+            torch.manual_seed(s_)
+            m = GCNdiff(adj, cfg)
+            m.eval()
+            ref_sd = {k: v.detach().numpy() for k, v in m.state_dict().items()}
+            shas[str(s_)] = state_dict_sha256(ref_sd)
+            assert shas[str(s_)] == state_dict_sha256(reference_init_state_dict(s_)), "restated initialisers drifted"
+            fixture(m, f"g9_refinit_seed{s_}.npz", 900 + s_, {"init_seed": s_})
+        meta["refinit_sha256"] = shas
+        sd7 = synthetic_state_dict(seed=7)
+        m7 = GCNdiff(adj, cfg)
+        m7.load_state_dict({k: torch.from_numpy(v) for k, v in sd7.items()})
+        m7.eval()
+        fixture(m7, "g10_synth_seed7.npz", 907, {"weights_seed": 7})
+        meta["seed7_weights_sha256"] = state_dict_sha256(sd7)
 
     with open(os.path.join(args.out, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
