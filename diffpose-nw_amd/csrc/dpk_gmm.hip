@@ -32,7 +32,12 @@ __device__ __forceinline__ double counter_uniform(uint64_t seed, uint64_t ctr) {
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
 
-__global__ void gmm_sample_kernel(const float* __restrict__ gmm, const float* __restrict__ poses3d, int n_src,
+// T: the dtype of the caller's arrays (float32, or float64 as numpy would hold them).  The choice
+// runs on double(p) either way (numpy converts p to double); with float64 arrays the root-relative
+// subtraction happens in double and only the outputs are rounded to float32, as the reference's
+// `.float()` at generators.py:46-50 does.
+template <typename T>
+__global__ void gmm_sample_kernel(const T* __restrict__ gmm, const T* __restrict__ poses3d, int n_src,
                                   int kn, const int64_t* __restrict__ index, int F, const double* __restrict__ u,
                                   uint64_t seed, double atol, float* __restrict__ uvxyz,
                                   float* __restrict__ noise_scale, int* __restrict__ status) {
@@ -42,11 +47,11 @@ __global__ void gmm_sample_kernel(const float* __restrict__ gmm, const float* __
     int64_t src = index ? index[f] : f;
     src %= n_src;                                    // generators.py:26-29 (index wraps)
     if (src < 0) src += n_src;
-    const float* row = gmm + ((size_t)src * J + j) * (size_t)kn * 5;
+    const T* row = gmm + ((size_t)src * J + j) * (size_t)kn * 5;
     // np.random.choice argument checks (mtrand.pyx): p >= 0, |kahan_sum(p) - 1| <= atol
     int flags = 0;
     double ksum = (double)row[0], c = 0.0;
-    if (row[0] < 0.f) flags |= 1;
+    if (row[0] < T(0)) flags |= 1;
     for (int k = 1; k < kn; ++k) {
         const double pk = (double)row[k * 5];
         if (pk < 0.0) flags |= 1;
@@ -69,33 +74,48 @@ __global__ void gmm_sample_kernel(const float* __restrict__ gmm, const float* __
     int idx = 0;
     for (int k = 0; k < kn; ++k) idx += (cdf[k] / last <= uu) ? 1 : 0;   // cdf is non-decreasing
     if (idx > kn - 1) idx = kn - 1;      // only reachable with invalid weights (flagged above)
-    const float* comp = row + idx * 5;
-    const float* p3 = poses3d + (size_t)src * J * 3;
+    const T* comp = row + idx * 5;
+    const T* p3 = poses3d + (size_t)src * J * 3;
     float* o = uvxyz + (size_t)gid * 5;
     float* s = noise_scale + (size_t)gid * 5;
-    o[0] = comp[1];
-    o[1] = comp[2];
-    s[0] = comp[3];
-    s[1] = comp[4];
+    o[0] = (float)comp[1];
+    o[1] = (float)comp[2];
+    s[0] = (float)comp[3];
+    s[1] = (float)comp[4];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        o[2 + d] = p3[j * 3 + d] - p3[d];           // root-relative, fp32 as numpy's float32 subtract
+        o[2 + d] = (float)(p3[j * 3 + d] - p3[d]);  // root-relative in the arrays' dtype, then .float()
         s[2 + d] = 1.0f;
     }
 }
 
 }  // namespace dpk_gmm
 
-extern "C" int dpk_gmm_sample(const float* gmm_dev, const float* poses3d_dev, int n_src, int kernel_n,
-                              const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
-                              float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream) {
+template <typename T>
+static int gmm_launch(const T* gmm_dev, const T* poses3d_dev, int n_src, int kernel_n, const int64_t* index_dev, int F,
+                      const double* u_dev, uint64_t seed, double atol, float* uvxyz_dev, float* noise_scale_dev,
+                      int* status_dev, void* stream) {
     if (F < 0 || n_src <= 0 || kernel_n < 1 || kernel_n > dpk_gmm::KMAX) return DPK_E_INVALID;
     if (F == 0) return DPK_OK;
     if (!gmm_dev || !poses3d_dev || !uvxyz_dev || !noise_scale_dev || !status_dev) return DPK_E_INVALID;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(status_dev, 0, sizeof(int), st) != hipSuccess) return DPK_E_HIP;
     const int n = F * dpk_gmm::J, nt = 256;
-    hipLaunchKernelGGL(dpk_gmm::gmm_sample_kernel, dim3((n + nt - 1) / nt), dim3(nt), 0, st, gmm_dev, poses3d_dev,
+    hipLaunchKernelGGL(dpk_gmm::gmm_sample_kernel<T>, dim3((n + nt - 1) / nt), dim3(nt), 0, st, gmm_dev, poses3d_dev,
                        n_src, kernel_n, index_dev, F, u_dev, seed, atol, uvxyz_dev, noise_scale_dev, status_dev);
     return hipGetLastError() == hipSuccess ? DPK_OK : DPK_E_HIP;
+}
+
+extern "C" int dpk_gmm_sample(const float* gmm_dev, const float* poses3d_dev, int n_src, int kernel_n,
+                              const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
+                              float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream) {
+    return gmm_launch(gmm_dev, poses3d_dev, n_src, kernel_n, index_dev, F, u_dev, seed, atol, uvxyz_dev,
+                      noise_scale_dev, status_dev, stream);
+}
+
+extern "C" int dpk_gmm_sample_f64(const double* gmm_dev, const double* poses3d_dev, int n_src, int kernel_n,
+                                  const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
+                                  float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream) {
+    return gmm_launch(gmm_dev, poses3d_dev, n_src, kernel_n, index_dev, F, u_dev, seed, atol, uvxyz_dev,
+                      noise_scale_dev, status_dev, stream);
 }

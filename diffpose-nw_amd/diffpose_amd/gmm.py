@@ -51,9 +51,13 @@ class PoseGeneratorGMM:
         assert p3.shape[0] == g.shape[0] and p3.shape[0] == len(self._actions)
         self.atol = numpy_atol(g.dtype)
         self.device = torch.device("cuda", 0) if device is None else torch.device(device)
-        # float32 on the device; the root-relative subtraction (generators.py:19) happens in the kernel
-        self._gmm = torch.from_numpy(np.ascontiguousarray(g, dtype=np.float32)).to(self.device)
-        self._p3 = torch.from_numpy(np.ascontiguousarray(p3, dtype=np.float32)).to(self.device)
+        # on the device in the arrays' own precision: float32, or float64 when either array is float64
+        # (numpy's choice runs on double(p) anyway; with float64 poses the root-relative subtraction,
+        # generators.py:19, runs in double and only the outputs are rounded, as the reference's .float())
+        self._f64 = g.dtype == np.float64 or p3.dtype == np.float64
+        dt = np.float64 if self._f64 else np.float32
+        self._gmm = torch.from_numpy(np.ascontiguousarray(g, dtype=dt)).to(self.device)
+        self._p3 = torch.from_numpy(np.ascontiguousarray(p3, dtype=dt)).to(self.device)
         self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     def __len__(self):
@@ -85,7 +89,8 @@ class PoseGeneratorGMM:
             else:
                 u_ptr, s = None, int(seed) & 0xFFFFFFFFFFFFFFFF
             st = torch.cuda.current_stream(self.device) if stream is None else stream
-            rc = _lib.lib().dpk_gmm_sample(self._gmm.data_ptr(), self._p3.data_ptr(), self._gmm.shape[0],
+            fn = _lib.lib().dpk_gmm_sample_f64 if self._f64 else _lib.lib().dpk_gmm_sample
+            rc = fn(self._gmm.data_ptr(), self._p3.data_ptr(), self._gmm.shape[0],
                                            self._kernel_n, idx_d.data_ptr(), F, u_ptr, s, self.atol,
                                            uv.data_ptr(), ns.data_ptr(), self._status.data_ptr(),
                                            ctypes.c_void_p(st.cuda_stream))

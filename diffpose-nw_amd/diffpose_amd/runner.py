@@ -19,6 +19,7 @@ Checkpoints load with ``torch.load(weights_only=True)``.
 from __future__ import annotations
 
 import logging
+import os
 import time
 import types
 
@@ -69,6 +70,7 @@ class Diffpose:
         self.num_timesteps = self.betas.shape[0]
         self.track_metrics = getattr(args, "track_metrics", False)
         self.inference_times, self.memory_usage = [], []
+        self.diffusion_step_count = []
         self.model_diff = self.model_pose = None
 
     def _adj(self):
@@ -103,6 +105,7 @@ class Diffpose:
         te = self.config.testing
         H = int(te.test_times)
         seq = self._seq()
+        self.diffusion_step_count = len(seq)        # runners/diffpose_frame.py:321
         if batches is None:
             batches = synthetic_eval_batches(n_frames, self.config.training.batch_size, seed=self.args.seed)
         root_mode = getattr(self.args, "root_mode", "quirk")
@@ -136,6 +139,38 @@ class Diffpose:
                 epoch_p1.update(float(np.mean(p1h)) * 1000.0, n)
                 epoch_p2.update(float(np.mean(p2h)) * 1000.0, n)
                 metrics.test_calculation(p1h, p2h, actions, err)
+        if self.track_metrics and self.inference_times:
+            # Final computational metrics (runners/diffpose_frame.py:407-409)
+            log_dir = getattr(self.args, "log_path", None)
+            self.log_performance_metrics(os.path.join(log_dir, "performance_metrics.txt") if log_dir else None)
         logging.info("sum (%d) | MPJPE: %.4f | P-MPJPE: %.4f", i + 1, epoch_p1.avg, epoch_p2.avg)
         self.epoch_loss = (epoch_p1.avg, epoch_p2.avg)
         return metrics.print_error(None, err, is_train)
+
+    def log_performance_metrics(self, output_path=None):
+        """Summary of the per-batch inference times and peak-memory deltas collected under
+        ``args.track_metrics``, logged and (with a path) written in the reference's file format
+        (runners/diffpose_frame.py:422-461).  Times cover pose model + sampler + metrics of a
+        batch here (one GPU pass); the reference's cover its generalized_steps call."""
+        if not self.track_metrics or not self.inference_times:
+            return
+        times, mem = self.inference_times, self.memory_usage
+        avg_time, max_time, min_time = sum(times) / len(times), max(times), min(times)
+        steps_data = f"Diffusion steps: {self.diffusion_step_count}"
+        if mem:
+            mem_data = f"Memory (MB): avg={sum(mem) / len(mem):.2f}, min={min(mem):.2f}, max={max(mem):.2f}"
+        else:
+            mem_data = "Memory: not tracked"
+        logging.info("=== Performance Summary ===")
+        logging.info(f"Time (s): avg={avg_time:.4f}, min={min_time:.4f}, max={max_time:.4f}")
+        logging.info(steps_data)
+        logging.info(mem_data)
+        if output_path:
+            with open(output_path, "w") as f:
+                f.write("=== Performance Metrics ===\n")
+                f.write(f"Time (s): avg={avg_time:.4f}, min={min_time:.4f}, max={max_time:.4f}\n")
+                f.write(f"{steps_data}\n")
+                f.write(f"{mem_data}\n")
+                f.write("\n=== Raw Data ===\n")
+                f.write(f"Times: {times}\n")
+                f.write(f"Memory: {mem}\n")

@@ -166,6 +166,13 @@ int dpk_gmm_sample(const float* gmm_dev, const float* poses3d_dev, int n_src, in
                    const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
                    float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream);
 
+/* The same for float64 arrays (numpy data kept in double): weights and poses are read as
+ * double, the root-relative subtraction runs in double and the outputs are rounded to float32 —
+ * the reference's order (generators.py:19 on the float64 array, .float() at :46-50). */
+int dpk_gmm_sample_f64(const double* gmm_dev, const double* poses3d_dev, int n_src, int kernel_n,
+                       const int64_t* index_dev, int F, const double* u_dev, uint64_t seed, double atol,
+                       float* uvxyz_dev, float* noise_scale_dev, int* status_dev, void* stream);
+
 /* GEMM arithmetic of the sampler's transformer/ResChebGC GEMMs (not part of the reference
  * interface; the reference computes everything in fp32 on its device):
  *   mode 0 (default): fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 accumulate;

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "diffpose_kernels.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(dpk_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(dpk_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exists():

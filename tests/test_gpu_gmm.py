@@ -108,3 +108,40 @@ def test_numpy_argument_errors():
     ds = PoseGeneratorGMM([np.zeros((2, 17, 3), np.float32)], [bad], [["a", "b"]], [np.zeros((2, 1), np.float32)])
     with pytest.raises(ValueError, match="sum to 1"):
         ds.batch([0, 1])
+
+
+def test_float64_inputs_follow_the_reference_dtype_order():
+    """float64 arrays (advisor r01): the choice runs on the float64 weights and the root-relative
+    subtraction in float64 before the .float() cast (generators.py:19, :46-50).  The weights are
+    built so that rounding them to float32 first would move a cdf boundary across the uniform,
+    and the poses so that subtract-then-round differs from round-then-subtract; the oracle's
+    numpy restatement (float64 throughout, as the reference) is matched bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from oracle.gmm_oracle import gmm_item
+    from diffpose_amd.gmm import numpy_atol
+
+    rng = np.random.Generator(np.random.PCG64(64))
+    F, kn = 40, 3
+    w = rng.dirichlet(np.ones(kn), size=(F, 17))
+    g = np.concatenate([w[..., None], rng.uniform(-1, 1, size=(F, 17, kn, 4))], axis=-1)
+    p3 = rng.normal(0.0, 0.5, size=(F, 17, 3)) + 1.0 / 3.0
+    u = rng.random((F, 17))
+    # put the uniform exactly on the float64 cdf boundary of joint 5 of frame 0: numpy picks the
+    # component past it; float32-rounded weights would move the boundary
+    c0 = w[0, 5, 0] / w[0, 5].sum()
+    u[0, 5] = c0
+    assert np.float64(np.float32(w[0, 5, 0])) != w[0, 5, 0]
+    ds = PoseGeneratorGMM([p3], [g], [["a"] * F], [np.zeros((F, 1))])
+    idx = np.arange(F)
+    uv, ns, *_ = ds.batch(idx, u=u)
+    p3rel = p3 - p3[:, :1]
+    atol = numpy_atol(np.float64)
+    for f in range(F):
+        ruv, rns = gmm_item(p3rel, g, f, u[f], atol)
+        assert np.array_equal(uv[f].cpu().numpy(), ruv), f
+        assert np.array_equal(ns[f].cpu().numpy(), rns), f
+    # the float32 path on the same data rounded to float32 differs somewhere in the poses
+    ds32 = PoseGeneratorGMM([p3.astype(np.float32)], [g.astype(np.float32)], [["a"] * F], [np.zeros((F, 1))])
+    uv32, *_ = ds32.batch(idx, u=u)
+    assert not torch.equal(uv32[..., 2:], uv[..., 2:])

@@ -178,3 +178,21 @@ def test_runner_test_hyber_vs_oracle():
         metrics.test_calculation(r1, r2, acts, err)
     q1, q2 = metrics.print_error(None, err, 1)
     assert abs(p1 - q1) <= 1e-4 and abs(p2 - q2) <= 1e-4, (p1, q1, p2, q2)
+
+
+def test_runner_track_metrics_writes_performance_file(tmp_path):
+    """args.track_metrics: per-batch times and peak-memory deltas are collected and written to
+    <log_path>/performance_metrics.txt in the reference's format (runners/diffpose_frame.py:407-461)."""
+    from diffpose_amd import runner
+    from diffpose_amd.data import synthetic_eval_batches
+
+    cfg = runner.default_config(test_times=1, test_timesteps=5, test_num_diffusion_timesteps=50, batch_size=16)
+    args = runner.default_args(track_metrics=True, log_path=str(tmp_path))
+    dp = runner.Diffpose(args, cfg, device="cuda:0")
+    dp.create_diffusion_model()
+    dp.create_pose_model()
+    dp.test_hyber(batches=list(synthetic_eval_batches(48, 16, seed=5)), is_train=1)
+    assert len(dp.inference_times) == 3 and len(dp.memory_usage) == 3
+    txt = (tmp_path / "performance_metrics.txt").read_text()
+    assert txt.startswith("=== Performance Metrics ===\nTime (s): avg=")
+    assert "Diffusion steps: 5\n" in txt and "Memory (MB): avg=" in txt and "=== Raw Data ===" in txt
