@@ -11,7 +11,8 @@ import os
 import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_kernels.hip")
+SRC = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_sampler.inc")
+KSRC = os.path.join(ROOT, "diffpose-nw_amd", "csrc", "dpk_kernels.hip")
 
 
 def main():
@@ -36,8 +37,12 @@ def main():
     body = s[b + 1:j]
     s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN" ::: "memory");' + body.replace("return;", 'asm volatile(";MARK_END" ::: "memory"); return;') \
         + '    asm volatile(";MARK_END" ::: "memory");\n' + s[j:]
-    tmp = "/tmp/isa_count.hip"
-    open(tmp, "w").write(s2)
+    # the device functions live in dpk_sampler.inc, included by dpk_kernels.hip: compile a copy of
+    # both from a scratch directory
+    os.makedirs("/tmp/isa_count", exist_ok=True)
+    open("/tmp/isa_count/dpk_sampler.inc", "w").write(s2)
+    tmp = "/tmp/isa_count/dpk_kernels.hip"
+    open(tmp, "w").write(open(KSRC).read())
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                     "-fno-slp-vectorize", f"-I{ROOT}/include", "-Wno-unused-result", "--cuda-device-only", "-S",
                     tmp, "-o", "/tmp/isa_count.s"], check=True, stderr=subprocess.DEVNULL)
