@@ -653,10 +653,20 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
             tpb = tpb_;
         }
         // nn.Linear weight is (out, in): W_eff[k][n] = weight[n][k]
-        pack_blocks(Lw + OFF_QKV, D, D3, KB_D, 18, [&](int k, int n) {
+        auto wqkv = [&](int k, int n) {
             const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
             return w[(n % D) * D + k];
-        });
+        };
+        // fp32 QKV GEMM with LN0's affine folded in (DPK_LN0_FOLD; the LN phase writes
+        // (x - mean) / (std + eps)): W' = diag(a) W, bias c = b W + b_qkv (summed in double)
+        const bool fold0 = DPK_LN0_FOLD && !DPK_LN_FUSE;
+        pack_blocks(Lw + OFF_QKV, D, D3, KB_D, 18, [&](int k, int n) { return fold0 ? n0a[k] * wqkv(k, n) : wqkv(k, n); });
+        for (int n = 0; n < D3; ++n) {
+            double cs = 0.0;
+            for (int k = 0; k < D; ++k) cs += (double)n0b[k] * (double)wqkv(k, n);
+            const float bqkv = n < D ? bq[n] : (n < 2 * D ? bk[n - D] : bv[n - 2 * D]);
+            Lw[OFF_CQKV + n] = (float)(cs + (double)bqkv);
+        }
         pack_blocks(Lw + OFF_O, D, D, KB_D, 6, [&](int k, int n) { return wo[n * D + k]; });
         pack_blocks(Lw + OFF_FC1, D, D2, KB_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
         pack_blocks(Lw + OFF_FC2, D2, D, KB_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
