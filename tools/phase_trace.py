@@ -26,6 +26,8 @@ def _events(gemm_mode="fp32", fused=None):
     # fp32 mode built with -DDPK_LN_FUSE=1: no LayerNorm phases (LN0 in the QKV operand, LN1 in graph1)
     if fused is None:
         fused = gemm_mode == "fp32" and os.environ.get("DPK_LN_FUSE", "0") == "1"
+    # fp32 mode with LN1 mapped wave = pose (DPK_LN1_POSE, the default): no barrier between LN1 and graph1
+    ln1pose = gemm_mode == "fp32" and not fused and os.environ.get("DPK_LN1_POSE", "1") == "1"
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
     npass = {"QKV": 3, "fc1": 2} if gemm_mode in ("f16x3", "bf16") else {}
@@ -40,9 +42,9 @@ def _events(gemm_mode="fp32", fused=None):
             bar(p + "LN0")
         gemm(p + "QKV"); bar(p + "QKV")
         bar(p + "attention"); gemm(p + "O"); bar(p + "O")
-        if not fused:
+        if not fused and not ln1pose:
             bar(p + "LN1")
-        bar(p + ("LN1+graph1" if fused else "graph1")); gemm(p + "fc1"); bar(p + "fc1")
+        bar(p + ("LN1+graph1" if fused or ln1pose else "graph1")); gemm(p + "fc1"); bar(p + "fc1")
         gemm(p + "fc2"); bar(p + "fc2")
         bar(p + "graph2+cheb1"); gemm(p + "C1"); bar(p + "C1")
         bar(p + "cheb_prep2"); gemm(p + "C2"); bar(p + "C2")
