@@ -111,6 +111,16 @@ def run(step=10, frames=1024, gemm_mode="fp32"):
             part = "after_epi"
         a = agg.setdefault(key, {})
         a[part] = a.get(part, 0.0) + float(d[:, :, k].max(1).mean())
+    # per-wave view: mean over workgroups of each wave's segments per phase (summed over layers),
+    # to expose imbalance between the 4 waves
+    perw = {}
+    for k in range(ne - 1):
+        name, kind = EVENTS[k + 1]
+        if kind not in ("pre", "loop", "epi"):
+            continue
+        key = name.split(".", 1)[1] if name.startswith("L") and "." in name else name
+        perw.setdefault(key, np.zeros(4))
+        perw[key] += d[:, :, k].mean(0)
     total = sum(sum(v.values()) for v in agg.values())
     print(f"kernel {ms:.3f} ms for {len(seq)} steps; traced step {step}: {step_cyc:.0f} cycles (sum of slowest-wave "
           f"segments {total:.0f}); implied clock {step_cyc / (ms / len(seq) * 1e-3) / 1e9:.2f} GHz")
@@ -119,6 +129,9 @@ def run(step=10, frames=1024, gemm_mode="fp32"):
     for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1].values())):
         tot = sum(v.values())
         print(f"{k:<14}" + "".join(f"{v.get(c, 0):>11.0f}" for c in cols) + f"{tot:>10.0f}{100 * tot / total:>7.1f}")
+    print("per-wave compute (loop + epilogue + compute segments, mean over workgroups):")
+    for k, v in perw.items():
+        print(f"  {k:<14}" + "".join(f"{x:>10.0f}" for x in v) + f"   spread {v.max() - v.min():>7.0f}")
     print(json.dumps({"step_cycles": step_cyc, "phases": {k: {c: round(x, 1) for c, x in v.items()} for k, v in agg.items()}}))
 
 
@@ -128,7 +141,10 @@ if __name__ == "__main__":
     ap.add_argument("--run", action="store_true")
     ap.add_argument("--step", type=int, default=10)
     ap.add_argument("--gemm", choices=("fp32", "f16x3", "bf16"), default="fp32")
+    ap.add_argument("--so", default=None, help="traced library to run (default build/trace/libdpk_trace.so)")
     a = ap.parse_args()
+    if a.so:
+        SO = a.so
     if a.build:
         build()
     if a.run:
