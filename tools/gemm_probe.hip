@@ -1,7 +1,7 @@
 // Microbenchmark of the sampler's GEMM phase in isolation (tools/gemm_probe.hip).
 // Includes the kernel source and times gemm_wave variants with s_memtime, one workgroup per CU,
 // every CU busy, ITER back-to-back calls separated by a workgroup barrier (as in the sampler).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -Iinclude \
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Iinclude \
 //        tools/gemm_probe.hip -o build/gemm_probe
 #include <hip/hip_runtime.h>
 // per-wave phase accounting: [0] barrier + prefetch + setup, [1] k-loop, [2] epilogue

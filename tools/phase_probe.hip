@@ -3,7 +3,7 @@
 // workgroup barrier the sampler puts after it; s_memtime per call (max over the 4 waves of
 // workgroup 0).  Phase 0 is the barrier alone.  Inputs are synthetic (LDS filled with small
 // values); only the timing is meaningful.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -Iinclude \
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form -Iinclude \
 //        tools/phase_probe.hip -o build/phase_probe        (-DPROBE_SRC=<kernel copy> for variants)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
