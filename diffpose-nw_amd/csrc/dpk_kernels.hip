@@ -83,6 +83,7 @@ struct SampleArgs {
     int H;                // pose: test_times
     int root_mode;        // pose: 0 reference in-place quirk (root zeroed), 1 root-relative, 2 raw
     unsigned mask;        // 17-bit key mask
+    const unsigned* pmask;  // per-pose 17-bit key masks [N] (dpk_set_pose_masks), or null: `mask` for all
     float eta;
     unsigned long long seed;
     int pose_off;         // first pose of this launch (a batch split over two launches, see launch_sampler)
@@ -221,6 +222,8 @@ struct dpk_handle {
     std::vector<float> h_temb;
     bool have_graph = false, have_weights = false;
     unsigned mask = (1u << J) - 1u;
+    const unsigned* pmask = nullptr;   // dpk_set_pose_masks: caller-owned device array
+    int pmask_n = 0;
     std::vector<float> h_adj;
     bool profiling = false;
     bool sparse_graph = false;     // adjacency matches the compiled H36M Chebyshev pattern
@@ -588,6 +591,22 @@ int dpk_set_mask(dpk_handle* h, const uint8_t* m) {
     return DPK_OK;
 }
 
+int dpk_set_pose_masks(dpk_handle* h, const uint32_t* bits_dev, int n) {
+    if (!h) return DPK_E_INVALID;
+    if (bits_dev && n <= 0) return fail(h, DPK_E_INVALID, "dpk_set_pose_masks: n must be positive");
+    h->pmask = reinterpret_cast<const unsigned*>(bits_dev);
+    h->pmask_n = bits_dev ? n : 0;
+    return DPK_OK;
+}
+
+// per-pose masks cover the launch's N poses (models/GraFormer.py:107-108 broadcasts [N,1,17])
+static int check_pose_masks(dpk_handle* h, int N, const char* who) {
+    if (h->pmask && N > h->pmask_n)
+        return fail(h, DPK_E_INVALID, std::string(who) + ": " + std::to_string(N) + " poses but dpk_set_pose_masks covers " +
+                                          std::to_string(h->pmask_n));
+    return DPK_OK;
+}
+
 int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const* ptrs, const int64_t* numels,
                      int n) {
     if (!h || !names || !ptrs || !numels || n <= 0) return fail(h, DPK_E_INVALID, "dpk_load_weights: bad args");
@@ -852,6 +871,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     int rc = check_ready(h);
     if (rc) return rc;
     if (N == 0) return DPK_OK;
+    if ((rc = check_pose_masks(h, N, "dpk_eps"))) return rc;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     bool cap = false;
@@ -888,6 +908,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     a.N = N;
     a.K = 1;
     a.mask = h->mask;
+    a.pmask = h->pmask;
     a.num_layers = h->num_layers;
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
@@ -908,6 +929,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     if (!sc) return fail(h, DPK_E_STATE, "schedule not set");
     if (N == 0) return DPK_OK;
     if (sc->tps_gen != h->weights_gen) return fail(h, DPK_E_STATE, "dpk_sample: schedule projections are stale");
+    if ((rc = check_pose_masks(h, N, "dpk_sample"))) return rc;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     bool cap = false;
@@ -926,6 +948,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     a.N = N;
     a.K = sc->K;
     a.mask = h->mask;
+    a.pmask = h->pmask;
     a.eta = sc->eta;
     a.seed = seed;
     a.num_layers = h->num_layers;
@@ -959,6 +982,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     int rc = check_ready(h, 1);
     if (rc) return rc;
     if (N == 0) return DPK_OK;
+    if ((rc = check_pose_masks(h, N, "dpk_pose"))) return rc;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     bool cap = false;
@@ -976,6 +1000,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     a.H = H;
     a.root_mode = root_mode;
     a.mask = h->mask;
+    a.pmask = h->pmask;
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");

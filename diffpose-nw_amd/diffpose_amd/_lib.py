@@ -16,7 +16,7 @@ DPK_OK = 0
 ERRORS = {-1: "DPK_E_INVALID", -2: "DPK_E_UNSUPPORTED", -3: "DPK_E_HIP", -4: "DPK_E_STATE", -5: "DPK_E_WEIGHTS"}
 
 # every symbol include/diffpose_kernels.h declares
-EXPORTS = ("dpk_version", "dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_schedule",
+EXPORTS = ("dpk_version", "dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks", "dpk_set_schedule",
            "dpk_eps", "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry", "dpk_last_error", "dpk_destroy")
 
 
@@ -52,6 +52,7 @@ def lib() -> ctypes.CDLL:
     L.dpk_set_graph.argtypes = [vp, fp]
     L.dpk_load_weights.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(fp), ctypes.POINTER(i64), i32]
     L.dpk_set_mask.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8)]
+    L.dpk_set_pose_masks.argtypes = [vp, vp, i32]
     L.dpk_set_schedule.argtypes = [vp, fp, i32, ctypes.POINTER(i32), i32, ctypes.c_float]
     L.dpk_eps.argtypes = [vp, vp, vp, vp, i32, vp]
     L.dpk_sample.argtypes = [vp, vp, vp, vp, vp, i32, u64, vp]
@@ -68,7 +69,7 @@ def lib() -> ctypes.CDLL:
     L.dpk_last_error.restype = ctypes.c_char_p
     L.dpk_destroy.argtypes = [vp]
     L.dpk_destroy.restype = None
-    for name in ("dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_schedule", "dpk_eps",
+    for name in ("dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks", "dpk_set_schedule", "dpk_eps",
                  "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry"):
         getattr(L, name).restype = i32
     _LIB = L

@@ -79,6 +79,7 @@ class _HipModel:
         _lib.check(h, "dpk_set_graph", L.dpk_set_graph(h, _f32p(self.adj)))
         self._mask_key = None
         self._mask_ref = None
+        self._pose_bits = None       # per-pose key masks (device int32 words), kept alive while bound
         self._sched_key = None
         self.training = False
 
@@ -117,18 +118,40 @@ class _HipModel:
 
     # -- mask -----------------------------------------------------------------------
     def set_mask(self, mask) -> None:
+        """Key mask as the reference's ``masked_fill(mask == 0, -1e9)`` (models/GraFormer.py:107-108):
+        one mask for every pose ((1,1,17) as runners/diffpose_frame.py:39-40 builds it, or any 17
+        entries), or one per pose ((N,1,17), broadcast over heads and queries like the reference's
+        ``mask.unsqueeze(1)``; the next call's batch must then have N poses)."""
+        L = _lib.lib()
+        if torch.is_tensor(mask) or isinstance(mask, np.ndarray):
+            shape = tuple(mask.shape)
+            if len(shape) == 3 and shape[0] != 1:
+                if shape[1:] != (1, self.n_pts):
+                    raise ValueError(f"a per-pose mask must be (N, 1, {self.n_pts}), got {shape}")
+                mt = torch.as_tensor(mask).to(self.device)
+                words = (mt.reshape(shape[0], self.n_pts) != 0).to(torch.int32)
+                shifts = torch.arange(self.n_pts, device=self.device, dtype=torch.int32)
+                bits = (words << shifts).sum(dim=1, dtype=torch.int32).contiguous()
+                _lib.check(self._h, "dpk_set_pose_masks", L.dpk_set_pose_masks(self._h, bits.data_ptr(), shape[0]))
+                self._pose_bits = bits
+                return
         if mask is None:
             m = np.ones(self.n_pts, dtype=np.uint8)
         else:
             mt = mask.detach().cpu() if torch.is_tensor(mask) else torch.as_tensor(np.asarray(mask))
-            if mt.dim() == 3 and mt.shape[0] != 1:
-                raise NotImplementedError("per-sample attention masks are not supported (the reference uses (1,1,17))")
             m = mt.reshape(-1).numpy().astype(np.uint8)
             if m.size != self.n_pts:
                 raise ValueError(f"mask must have {self.n_pts} key entries, got {m.size}")
         m = np.ascontiguousarray(m)
-        L = _lib.lib()
         _lib.check(self._h, "dpk_set_mask", L.dpk_set_mask(self._h, m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        if self._pose_bits is not None:
+            _lib.check(self._h, "dpk_set_pose_masks", L.dpk_set_pose_masks(self._h, None, 0))
+            self._pose_bits = None
+
+    def _check_mask_batch(self, n: int) -> None:
+        """A per-pose mask broadcasts only against a batch of its own size (torch broadcasting)."""
+        if self._pose_bits is not None and self._pose_bits.numel() != n:
+            raise ValueError(f"per-pose mask has {self._pose_bits.numel()} poses, the batch {n}")
 
     def _sync_mask(self, mask) -> None:
         """Upload the key mask when it changed.  Cached by object identity + in-place version;
@@ -216,6 +239,7 @@ class HipGCNdiff(_HipModel):
         if t.numel() != n:
             raise ValueError(f"t must have {n} entries, got {t.numel()}")
         self._sync_mask(mask)
+        self._check_mask_batch(n)
         eps = torch.empty_like(x)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = _lib.lib()
@@ -232,6 +256,7 @@ class HipGCNdiff(_HipModel):
         self.set_schedule(seq, betas, eta)
         self._sync_mask(mask)
         n = x.shape[0]
+        self._check_mask_batch(n)
         out = torch.empty_like(x) if out is None else out
         xs = x0s = None
         if trajectory:

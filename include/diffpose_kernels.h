@@ -88,6 +88,15 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
  * masked_fill(-1e9) path of models/GraFormer.py:107-108. */
 int dpk_set_mask(dpk_handle* h, const uint8_t* mask_host);
 
+/* Per-pose key masks: the reference's masked_fill broadcasts a [N,1,n_pts] mask
+ * over heads and queries (models/GraFormer.py:107-108, mask.unsqueeze(1)).
+ * bits_dev: n uint32 words in device memory, bit j of word i = key j of pose i
+ * attends.  Owned by the caller and read by every later dpk_eps / dpk_sample /
+ * dpk_pose launch (pose i of the launch uses word i; a launch of more than n
+ * poses fails with DPK_E_INVALID) until replaced; NULL returns to the
+ * dpk_set_mask mask for all poses. */
+int dpk_set_pose_masks(dpk_handle* h, const uint32_t* bits_dev, int n);
+
 /* DDIM schedule.  alpha_bar: fp32 table (1-cat([0],betas)).cumprod(0), n_alpha = T+1
  * entries (compute_alpha, common/utils_diff.py:40-43); seq: K timesteps in
  * ascending order as built by test_hyber (runners/diffpose_frame.py:310-317);

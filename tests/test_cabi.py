@@ -54,6 +54,7 @@ def test_argument_validation_without_gpu():
     bad_pose = _lib.DpkConfig(96, 5, 4, 17, 3, 3, 0)        # coords other than [5,5] / [2,3]
     assert L.dpk_create(ctypes.byref(bad_pose), ctypes.byref(h)) == -2
     assert L.dpk_pose(None, None, None, None, 0, 1, 0, None) == -1
+    assert L.dpk_set_pose_masks(None, None, 0) == -1
     # num_layers is a run-time value in 1..5 (config num_layer); 0 and 6 are rejected before any
     # device call, 3 passes the shape check and only then needs a device (none here: DPK_E_HIP)
     for nl, rc in ((0, -2), (6, -2), (3, -3)):

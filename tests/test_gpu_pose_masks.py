@@ -1,0 +1,142 @@
+"""Per-pose attention key masks: the reference's ``scores.masked_fill(mask == 0, -1e9)`` with a
+[N,1,17] mask broadcast over heads and queries (models/GraFormer.py:107-108, ``mask.unsqueeze(1)``),
+through dpk_set_pose_masks.
+
+  * vs the golden-pinned oracle (the same masked_fill on the same per-pose mask): one denoiser
+    call within EPS_TOL, a K=10 DDIM trajectory's final x within TRAJ_TOL (the bars of
+    test_gpu_parity.py);
+  * bitwise: each pose of a per-pose-masked batch equals the same pose of a batch run with its
+    mask as the handle-wide one (same launch geometry, only the mask's source differs);
+  * a batch whose size differs from the mask's is rejected (Python: ValueError, C ABI:
+    DPK_E_INVALID), and a later (1,1,17) mask restores the handle-wide path.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from diffpose_amd import _lib
+from diffpose_amd.data import synthetic_batch
+from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
+from diffpose_amd.schedule import get_beta_schedule, make_seq
+from diffpose_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+EPS_TOL = 2e-5
+TRAJ_TOL = 2e-5
+
+
+def _betas(T):
+    return torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
+                                              num_diffusion_timesteps=T)).float()
+
+
+@pytest.fixture(scope="module")
+def model():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    m = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+    m.load_state_dict(synthetic_state_dict())
+    return m
+
+
+def _masks(n, seed=5):
+    """n key masks: all ones, single keys, the root only dropped, and random patterns (every
+    mask keeps at least one key, as a softmax row needs)."""
+    rng = np.random.default_rng(seed)
+    m = rng.random((n, 1, 17)) < 0.6
+    m[0] = True
+    m[1] = False
+    m[1, 0, 16] = True          # key 16 alone (the VALU border key)
+    m[2] = False
+    m[2, 0, 3] = True           # one MFMA key alone
+    m[3] = True
+    m[3, 0, 0] = False
+    for i in range(n):
+        if not m[i].any():
+            m[i, 0, i % 17] = True
+    return torch.from_numpy(m)
+
+
+def _maxdiff(a, b):
+    return float((a.detach().cpu().double() - b.detach().cpu().double()).abs().max())
+
+
+def test_eps_per_pose_masks_vs_oracle(model):
+    from oracle import gcndiff_oracle as O
+
+    n = 12
+    x, _ = synthetic_batch(n, seed=21)
+    x = torch.from_numpy(x)
+    t = torch.arange(n, dtype=torch.float32) * 4.0
+    m = _masks(n)
+    eps = model(x.cuda(), m.cuda(), t.cuda(), 0)
+    ref = O.gcndiff_forward(O.params_to_torch(synthetic_state_dict()), O.adjacency(), x, m, t)
+    assert _maxdiff(eps, ref) <= EPS_TOL
+    # the masks matter: the all-ones run differs for the masked poses
+    ones = model(x.cuda(), torch.ones(1, 1, 17, dtype=torch.bool, device="cuda:0"), t.cuda(), 0)
+    assert _maxdiff(ones[1:3], eps[1:3]) > 1e-3
+    assert torch.equal(ones[0], eps[0])
+
+
+def test_sample_per_pose_masks_vs_oracle(model):
+    from oracle import gcndiff_oracle as O
+
+    n = 16
+    x, _ = synthetic_batch(n, seed=22)
+    x = torch.from_numpy(x)
+    seq = make_seq("uniform", 50, 10)
+    m = _masks(n, seed=9)
+    out = model.sample(x.cuda(), seq, _betas(51), mask=m.cuda())
+    P = O.params_to_torch(synthetic_state_dict())
+    adj = O.adjacency()
+    xs, _ = O.generalized_steps(x, m, seq, lambda a, mm, tt: O.gcndiff_forward(P, adj, a, mm, tt), _betas(51))
+    assert _maxdiff(out, xs[-1]) <= TRAJ_TOL
+
+
+def test_per_pose_masks_bitwise_vs_handle_mask(model):
+    """Two mask patterns alternating over 64 poses: each pose equals the same pose of the batch
+    run with its pattern as the handle-wide mask."""
+    n = 64
+    x, _ = synthetic_batch(n, seed=23)
+    x = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, 10)
+    a = torch.ones(1, 1, 17, dtype=torch.bool)
+    b = torch.ones(1, 1, 17, dtype=torch.bool)
+    b[0, 0, [0, 5, 16]] = False
+    per = torch.where((torch.arange(n) % 2 == 0).view(n, 1, 1), a, b).cuda()
+    out = model.sample(x, seq, _betas(51), mask=per)
+    out_a = model.sample(x, seq, _betas(51), mask=a.cuda())
+    out_b = model.sample(x, seq, _betas(51), mask=b.cuda())
+    assert torch.equal(out[0::2], out_a[0::2])
+    assert torch.equal(out[1::2], out_b[1::2])
+    assert not torch.equal(out_a[1::2], out_b[1::2])
+
+
+def test_per_pose_mask_batch_checks(model):
+    x, _ = synthetic_batch(8, seed=24)
+    x = torch.from_numpy(x).cuda()
+    t = torch.full((8,), 7.0, device="cuda:0")
+    with pytest.raises(ValueError):
+        model(x, _masks(4).cuda(), t, 0)
+    with pytest.raises(ValueError):
+        model(x, torch.ones(8, 17, 17, dtype=torch.bool, device="cuda:0"), t, 0)
+    # C ABI: masks for 4 poses, a launch of 8
+    bits = torch.full((4,), (1 << 17) - 1, dtype=torch.int32, device="cuda:0")
+    L = _lib.lib()
+    assert L.dpk_set_pose_masks(model._h, bits.data_ptr(), 4) == 0
+    eps = torch.empty_like(x)
+    stream = torch.cuda.current_stream().cuda_stream
+    rc = L.dpk_eps(model._h, x.data_ptr(), t.data_ptr(), eps.data_ptr(), 8, stream)
+    assert rc == -1 and b"dpk_set_pose_masks covers 4" in L.dpk_last_error(model._h)
+    assert L.dpk_set_pose_masks(model._h, None, 0) == 0
+    model._pose_bits = None
+    model._mask_key = model._mask_ref = None
+    # back on the handle-wide mask: equal to a fresh all-ones run
+    ones = torch.ones(1, 1, 17, dtype=torch.bool, device="cuda:0")
+    e1 = model(x, _masks(8).cuda(), t, 0)
+    e2 = model(x, ones, t, 0)
+    e3 = model(x, None, t, 0)
+    assert torch.equal(e2, e3) and not torch.equal(e1, e2)
