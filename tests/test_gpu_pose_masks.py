@@ -140,3 +140,25 @@ def test_per_pose_mask_batch_checks(model):
     e2 = model(x, ones, t, 0)
     e3 = model(x, None, t, 0)
     assert torch.equal(e2, e3) and not torch.equal(e1, e2)
+
+
+def test_gcnpose_per_pose_masks_vs_oracle():
+    """GCNpose.forward(x, mask) with a [N,1,17] mask (dpk_pose reads the same per-pose words)."""
+    from oracle import gcndiff_oracle as O
+    from diffpose_amd.gcnpose import HipGCNpose
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    pm = HipGCNpose(adj_mx_from_edges(), None, device="cuda:0")
+    pm.load_state_dict(synthetic_state_dict(kind="pose"))
+    n = 10
+    x, _ = synthetic_batch(n, seed=25)
+    x2d = torch.from_numpy(np.ascontiguousarray(x[:, :, :2]))
+    m = _masks(n, seed=13)
+    xyz = pm(x2d.cuda(), m.cuda())
+    ref = O.gcnpose_forward(O.params_to_torch(synthetic_state_dict(kind="pose")), O.adjacency(), x2d, m)
+    assert _maxdiff(xyz, ref) <= 2e-5          # POSE_TOL of test_gpu_pose_metrics.py
+    ones = pm(x2d.cuda(), torch.ones(1, 1, 17, dtype=torch.bool, device="cuda:0"))
+    assert torch.equal(ones[0], xyz[0]) and _maxdiff(ones[1:3], xyz[1:3]) > 1e-4
+    with pytest.raises(ValueError):
+        pm(x2d.cuda(), _masks(4).cuda())
