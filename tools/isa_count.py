@@ -44,7 +44,7 @@ def main():
     tmp = "/tmp/isa_count/dpk_kernels.hip"
     open(tmp, "w").write(open(KSRC).read())
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                    "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-misched-cluster=0", f"-I{ROOT}/include", "-Wno-unused-result", "--cuda-device-only", "-S",
+                    "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-misched-cluster=0", "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1", f"-I{ROOT}/include", "-Wno-unused-result", "--cuda-device-only", "-S",
                     tmp, "-o", "/tmp/isa_count.s"], check=True, stderr=subprocess.DEVNULL)
     asm = open("/tmp/isa_count.s").read()
     k = asm.index(a.kernel)

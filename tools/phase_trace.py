@@ -56,7 +56,7 @@ def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
     src = [os.path.join(ROOT, "diffpose-nw_amd", "csrc", f) for f in ("dpk_kernels.hip", "dpk_metrics.hip", "dpk_gmm.hip")]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-misched-cluster=0", "-Wno-unused-result", f"-I{ROOT}/include", "-DDPK_TRACE=1"] + src + ["-o", SO]
+           "-ffp-contract=off", "-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-misched-cluster=0", "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1", "-Wno-unused-result", f"-I{ROOT}/include", "-DDPK_TRACE=1"] + src + ["-o", SO]
     cmd += os.environ.get("DPK_TRACE_EXTRA", "").split()
     subprocess.run(cmd, check=True)
     print("built", SO)
