@@ -298,13 +298,17 @@ def rank_main(args):
     out = torch.empty_like(x)
     rows = x.shape[0]
     model = None
+    setup_ms = None
     if not dry:
         from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
         from diffpose_amd.weights import synthetic_state_dict
 
         model = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
         model.load_state_dict(synthetic_state_dict())
-        model.set_schedule(seq, betas, args.eta)
+        sync()
+        t_set = time.perf_counter()
+        model.set_schedule(seq, betas, args.eta)       # host-synchronous: the call returns with it built
+        setup_ms = (time.perf_counter() - t_set) * 1e3
 
     gathered = {}
 
@@ -444,6 +448,12 @@ def rank_main(args):
                    "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if use_dist else ""),
                    "hipgraph": bool(args.graph), "gemm": args.gemm},
         "per_rank_ms": per_rank_ms,
+        "setup_ms": None if setup_ms is None else round(setup_ms, 4),
+        "setup_note": None if setup_ms is None else (
+            f"per (weights, schedule), outside the timed region: dpk_set_schedule's host step scalars, upload and "
+            f"temb_kernel ({K} workgroups: the timestep MLP and the 5 temb_proj rows of every step, batch-invariant, "
+            f"SURVEY a7), host-synchronous wall time; every dpk_sample with that schedule reuses them, so a caller "
+            f"running a single batch pays it once on top of ms_per_step"),
         "roofline": roof,
         "cpu_baseline": None,
     }

@@ -189,8 +189,13 @@ struct Sched {
     std::vector<std::pair<hipStream_t, hipEvent_t>> uses;   // last launch on each stream
 };
 
-// dpk_eps's per-pose projections [N][NL][D], one buffer per caller stream: two dpk_eps calls on
-// different streams never share one, and calls on the same stream are ordered by the stream
+// dpk_eps's per-pose projections [N][NL][D].  Uncaptured calls use one buffer per caller stream:
+// two dpk_eps calls on different streams never share one, and calls on the same stream are ordered
+// by the stream, so a buffer can grow (after a sync of its stream) without racing anyone.  A
+// captured call becomes a graph node that keeps the buffer's address for the graph's life and may
+// replay on any stream, concurrently with other graphs: it takes a buffer of its own, the handle's
+// spare (allocated by the uncaptured calls, since nothing can be allocated inside a capture), and
+// that buffer is pinned until dpk_destroy.
 struct EpsBuf {
     hipStream_t st = nullptr;
     float* p = nullptr;
@@ -211,7 +216,9 @@ struct dpk_handle {
     uint64_t weights_gen = 0;      // bumped by every weight/graph upload
     Sched* sched = nullptr;        // current schedule
     std::vector<Sched*> retired;   // replaced schedules not yet known to be unused
-    std::vector<EpsBuf> eps_bufs;
+    std::vector<EpsBuf> eps_bufs;  // per stream (uncaptured dpk_eps)
+    EpsBuf eps_spare;              // unused buffer for the next captured dpk_eps (no stream)
+    std::vector<float*> eps_pinned;   // buffers owned by captured dpk_eps launches (freed at destroy)
     std::vector<float> h_arena;    // host staging of the arena
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
@@ -412,6 +419,9 @@ static int upload(dpk_handle* h) {
     // launches already enqueued on any stream may still read the arena: overwrite it only after
     // the device has drained (weights and graphs are loaded rarely; the launches stay async)
     HIPCHK(h, hipDeviceSynchronize());
+    // every uncaptured launch has completed: the retired schedules only they used go now, so the
+    // projections below are recomputed for the current schedule and the graph-pinned ones only
+    sched_sweep(h);
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
     if (!h->arena16) HIPCHK(h, hipMalloc(&h->arena16, (size_t)ARENA16_BYTES));
     HIPCHK(h, hipMemcpy(h->arena16, h->h_arena16.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
@@ -542,6 +552,8 @@ void dpk_destroy(dpk_handle* h) {
     for (Sched* s : h->retired) sched_free(s);
     for (auto& b : h->eps_bufs)
         if (b.p) (void)hipFree(b.p);
+    if (h->eps_spare.p) (void)hipFree(h->eps_spare.p);
+    for (float* p : h->eps_pinned) (void)hipFree(p);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     for (auto* v : {&h->ev_used, &h->ev_free})
         for (auto& e : *v) {
@@ -877,32 +889,50 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     bool cap = false;
     rc = capturing(h, st, &cap);
     if (rc) return rc;
-    EpsBuf* buf = nullptr;
-    for (auto& b : h->eps_bufs)
-        if (b.st == st) buf = &b;
-    if (!buf) {
-        h->eps_bufs.push_back(EpsBuf{st, nullptr, 0});
-        buf = &h->eps_bufs.back();
+    float* proj = nullptr;
+    if (cap) {
+        // a graph node keeps this buffer: take the spare (sized by earlier uncaptured calls) for good
+        if (h->eps_spare.cap < N)
+            return fail(h, DPK_E_STATE, "dpk_eps: a captured call needs a projection buffer of " + std::to_string(N) +
+                                            " poses, and the spare holds " + std::to_string(h->eps_spare.cap) +
+                                            "; make an uncaptured dpk_eps call of >= N poses before each capture");
+        proj = h->eps_spare.p;
+        h->eps_pinned.push_back(proj);
+        h->eps_spare = EpsBuf{};
+    } else {
+        EpsBuf* buf = nullptr;
+        for (auto& b : h->eps_bufs)
+            if (b.st == st) buf = &b;
+        if (!buf) {
+            h->eps_bufs.push_back(EpsBuf{st, nullptr, 0});
+            buf = &h->eps_bufs.back();
+        }
+        if (buf->cap < N) {
+            // earlier dpk_eps calls on this stream may still read the old buffer
+            HIPCHK(h, hipStreamSynchronize(st));
+            if (buf->p) HIPCHK(h, hipFree(buf->p));
+            buf->p = nullptr;
+            buf->cap = 0;
+            const int cap_new = std::max(N, 64);
+            HIPCHK(h, hipMalloc(&buf->p, (size_t)cap_new * NL * D * 4));
+            buf->cap = cap_new;
+        }
+        proj = buf->p;
+        // keep a spare of at least N poses for a later capture (no launch has seen it: no race)
+        if (h->eps_spare.cap < N) {
+            if (h->eps_spare.p) HIPCHK(h, hipFree(h->eps_spare.p));
+            h->eps_spare = EpsBuf{};
+            const int cap_new = std::max(N, 64);
+            HIPCHK(h, hipMalloc(&h->eps_spare.p, (size_t)cap_new * NL * D * 4));
+            h->eps_spare.cap = cap_new;
+        }
     }
-    if (buf->cap < N) {
-        if (cap)
-            return fail(h, DPK_E_STATE, "dpk_eps: this stream's projection buffer holds " + std::to_string(buf->cap) +
-                                            " poses; size it with an uncaptured call of >= N poses before capturing");
-        // earlier dpk_eps calls on this stream may still read the old buffer
-        HIPCHK(h, hipStreamSynchronize(st));
-        if (buf->p) HIPCHK(h, hipFree(buf->p));
-        buf->p = nullptr;
-        buf->cap = 0;
-        const int cap_new = std::max(N, 64);
-        HIPCHK(h, hipMalloc(&buf->p, (size_t)cap_new * NL * D * 4));
-        buf->cap = cap_new;
-    }
-    hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(256), 0, st, h->temb, t, 1, buf->p);
+    hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(256), 0, st, h->temb, t, 1, proj);
     HIPCHK(h, hipGetLastError());
     SampleArgs a{};
     a.arena = h->arena;
     a.coef = nullptr;     // unused in eps mode
-    a.tproj = buf->p;
+    a.tproj = proj;
     a.x_in = x;
     a.x_out = eps;
     a.N = N;

@@ -80,6 +80,7 @@ class _HipModel:
         self._mask_key = None
         self._mask_ref = None
         self._pose_bits = None       # per-pose key masks (device int32 words), kept alive while bound
+        self._mask_hold = []         # per-pose mask arrays a captured graph reads (kept until close)
         self._sched_key = None
         self.training = False
 
@@ -153,6 +154,20 @@ class _HipModel:
         if self._pose_bits is not None and self._pose_bits.numel() != n:
             raise ValueError(f"per-pose mask has {self._pose_bits.numel()} poses, the batch {n}")
 
+    def _note_mask_use(self) -> None:
+        """Before a launch that reads the per-pose mask array by address (dpk_set_pose_masks):
+        a captured launch keeps that address for the graph's life, so the array is held until
+        close(); an eager launch on another stream than the one that allocated it must not see
+        the caching allocator hand the memory out again while it runs (record_stream)."""
+        bits = self._pose_bits
+        if bits is None:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            if not any(b is bits for b in self._mask_hold):
+                self._mask_hold.append(bits)
+        else:
+            bits.record_stream(torch.cuda.current_stream(self.device))
+
     def _sync_mask(self, mask) -> None:
         """Upload the key mask when it changed.  Cached by object identity + in-place version;
         the cached object is kept alive so its id cannot be recycled by a new tensor."""
@@ -200,6 +215,7 @@ class _HipModel:
         h, self._h = getattr(self, "_h", None), None
         if h:
             _lib.lib().dpk_destroy(h)
+        self._mask_hold = []
 
     def __del__(self):
         try:
@@ -240,6 +256,7 @@ class HipGCNdiff(_HipModel):
             raise ValueError(f"t must have {n} entries, got {t.numel()}")
         self._sync_mask(mask)
         self._check_mask_batch(n)
+        self._note_mask_use()
         eps = torch.empty_like(x)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = _lib.lib()
@@ -257,6 +274,7 @@ class HipGCNdiff(_HipModel):
         self._sync_mask(mask)
         n = x.shape[0]
         self._check_mask_batch(n)
+        self._note_mask_use()
         out = torch.empty_like(x) if out is None else out
         xs = x0s = None
         if trajectory:

@@ -47,6 +47,7 @@ class HipGCNpose(_HipModel):
     def _launch(self, x2d, mask, xyz, uvxyz, test_times: int, root_mode) -> None:
         self._sync_mask(mask)
         self._check_mask_batch(x2d.shape[0])
+        self._note_mask_use()
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = _lib.lib()
         rc = L.dpk_pose(self._h, x2d.data_ptr(), xyz.data_ptr() if xyz is not None else None,

@@ -20,15 +20,21 @@
  *   - Stream order: launches (dpk_sample / dpk_eps / dpk_pose / dpk_ddim_update) may be in
  *     flight on several streams at once.  dpk_set_schedule never rewrites a schedule a launch
  *     may still read: it builds a new one, and the old one is freed only after every stream
- *     that used it has passed its last launch.  dpk_eps keeps its per-pose timestep
- *     projections in a buffer per caller stream.  dpk_load_weights / dpk_set_graph wait for
- *     the device to drain before overwriting the weights (they are configuration calls).
+ *     that used it has passed its last launch.  Uncaptured dpk_eps calls keep their per-pose
+ *     timestep projections in a buffer per caller stream.  dpk_load_weights / dpk_set_graph
+ *     wait for the device to drain before overwriting the weights (configuration calls).
  *   - Graph capture (hipStreamBeginCapture / torch.cuda.graph): dpk_sample, dpk_eps, dpk_pose
  *     and dpk_ddim_update may be captured.  A captured launch reads the schedule current at
  *     capture time for the graph's whole life (a later dpk_set_schedule builds a new one and
  *     leaves the captured one in place; it is freed by dpk_destroy); weights reloaded later
- *     are seen by replays.  Nothing is allocated inside a captured call: dpk_eps needs one
- *     uncaptured call of at least N poses on the stream first (else DPK_E_STATE).
+ *     are seen by replays.  It also keeps the key mask it was captured with: the
+ *     dpk_set_mask bits by value, and the dpk_set_pose_masks array by address (that array
+ *     must stay allocated and unchanged while the graph may replay).  Nothing is allocated
+ *     inside a captured call: each captured dpk_eps takes a projection buffer of its own
+ *     (kept until dpk_destroy, so graphs captured on one stream can replay concurrently and
+ *     later uncaptured calls of any size cannot disturb them); that buffer comes from a spare
+ *     which every uncaptured dpk_eps of at least N poses refills, so one such call must come
+ *     before each capture (else DPK_E_STATE).
  */
 #ifndef DIFFPOSE_KERNELS_H
 #define DIFFPOSE_KERNELS_H
@@ -94,7 +100,9 @@ int dpk_set_mask(dpk_handle* h, const uint8_t* mask_host);
  * attends.  Owned by the caller and read by every later dpk_eps / dpk_sample /
  * dpk_pose launch (pose i of the launch uses word i; a launch of more than n
  * poses fails with DPK_E_INVALID) until replaced; NULL returns to the
- * dpk_set_mask mask for all poses. */
+ * dpk_set_mask mask for all poses.  The launches read the array asynchronously, on
+ * their streams: free or rewrite it only after they have completed (and never while
+ * a graph captured with it may replay). */
 int dpk_set_pose_masks(dpk_handle* h, const uint32_t* bits_dev, int n);
 
 /* DDIM schedule.  alpha_bar: fp32 table (1-cat([0],betas)).cumprod(0), n_alpha = T+1

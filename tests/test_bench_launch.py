@@ -45,3 +45,20 @@ def test_bench_refuses_world_size_mismatch():
     assert rc != 0
     assert line is None
     assert "WORLD_SIZE" in err
+
+
+def test_bench_config4_eight_ranks_cpu_dry():
+    """BASELINE config 4 (8,192 frames, 1,024 per GPU, 8 GPUs): the launcher starts 8 ranks, each
+    takes its shard_frames(8192, 8, r) range, and rank 0 reassembles the whole batch through the
+    all-gather (gloo here; RCCL on the node).  The same code path the driver's 8-GPU run takes,
+    minus the HIP sampler (runners/diffpose_frame.py:126-127, 342)."""
+    rc, line, err = _run(["--gpus", "8", "--config", "4", "--cpu-dry", "--steps", "2", "--warmup", "1"],
+                         timeout=420)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 8
+    assert line["scaling"] == "weak"
+    assert line["config"]["baseline_config"] == 4
+    assert line["config"]["frames_total"] == 8192 and line["config"]["frames_per_gpu"] == 1024
+    assert len(line["per_rank_ms"]) == 8
+    assert line["reassembly_ok"] is True
+    assert line["allgather_ms"] > 0

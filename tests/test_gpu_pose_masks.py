@@ -162,3 +162,69 @@ def test_gcnpose_per_pose_masks_vs_oracle():
     assert torch.equal(ones[0], xyz[0]) and _maxdiff(ones[1:3], xyz[1:3]) > 1e-4
     with pytest.raises(ValueError):
         pm(x2d.cuda(), _masks(4).cuda())
+
+
+@pytest.mark.parametrize("mode", ["eps", "sample"])
+def test_per_pose_masks_both_tile_sizes(model, mode):
+    """N = 1,100 poses: one full round of 4-pose workgroups (poses 0..1023, the 4-pose kernel's
+    mask word wave / (NW/P) with pose_off 0) and a tail of 76 poses in 2-pose workgroups (the
+    second launch, pose_off 1024).  Four mask patterns in an irregular order: every pose equals
+    the same pose of the batch run with its pattern as the handle-wide mask, bitwise (same
+    launch geometry, only the mask's source differs)."""
+    n = 1100
+    x, _ = synthetic_batch(n, seed=26)
+    x = torch.from_numpy(x).cuda()
+    pats = torch.ones(4, 1, 17, dtype=torch.bool)
+    pats[1, 0, [0, 5, 16]] = False
+    pats[2, 0, :16] = False                    # key 16 alone
+    pats[3, 0, 1::2] = False
+    which = torch.from_numpy((np.arange(n) * 7 + np.arange(n) // 5) % 4)
+    per = pats[which].cuda()
+    t = (torch.arange(n, dtype=torch.float32) % 50).cuda()
+    seq = make_seq("uniform", 50, 10)
+
+    def run(mask):
+        if mode == "eps":
+            return model(x, mask, t, 0)
+        return model.sample(x, seq, _betas(51), mask=mask)
+
+    out = run(per)
+    for k in range(4):
+        ref = run(pats[k : k + 1].cuda())
+        sel = (which == k).nonzero().flatten().cuda()
+        assert torch.equal(out[sel], ref[sel]), (mode, k)
+    head = (which[:1024] == 2).nonzero().flatten()
+    tail = 1024 + (which[1024:] == 2).nonzero().flatten()
+    assert head.numel() > 0 and tail.numel() > 0   # the key-16-alone pattern lands in both tile sizes
+
+
+def test_per_pose_masks_under_graph_capture(model):
+    """A captured sampler keeps reading the per-pose mask array it was captured with: replacing
+    the mask afterwards (and churning the caching allocator) does not change the replay."""
+    n = 40
+    x, _ = synthetic_batch(n, seed=27)
+    x = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, 10)
+    m1 = _masks(n, seed=31).cuda()
+    m2 = _masks(n, seed=32).cuda()
+    ref1 = model.sample(x, seq, _betas(51), mask=m1).clone()
+    ref2 = model.sample(x, seq, _betas(51), mask=m2).clone()
+    assert not torch.equal(ref1, ref2)
+    out = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        model.sample(x, seq, _betas(51), mask=m1, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        model.sample(x, seq, _betas(51), mask=m1, out=out)
+    assert torch.equal(model.sample(x, seq, _betas(51), mask=m2), ref2)    # a new mask array bound
+    junk = [torch.zeros(n, dtype=torch.int32, device="cuda:0") for _ in range(64)]   # reuse bait
+    for _ in range(2):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref1)
+    del junk, g

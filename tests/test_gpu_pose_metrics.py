@@ -182,8 +182,13 @@ def test_runner_test_hyber_vs_oracle():
 
 def test_runner_track_metrics_writes_performance_file(tmp_path):
     """args.track_metrics: per-batch times and peak-memory deltas are collected and written to
-    <log_path>/performance_metrics.txt in the reference's format (runners/diffpose_frame.py:407-461)."""
-    from diffpose_amd import runner
+    <log_path>/performance_metrics.txt in the reference's format (runners/diffpose_frame.py:407-461).
+    The timed window is the sampler call alone, as the reference's (:345-370: start after the pose
+    model, stop after generalized_steps and a device sync): a pose model and a metrics step made
+    0.25 s slower show up in pose_times / metrics_times and not in inference_times."""
+    import time
+
+    from diffpose_amd import metrics, runner
     from diffpose_amd.data import synthetic_eval_batches
 
     cfg = runner.default_config(test_times=1, test_timesteps=5, test_num_diffusion_timesteps=50, batch_size=16)
@@ -191,8 +196,31 @@ def test_runner_track_metrics_writes_performance_file(tmp_path):
     dp = runner.Diffpose(args, cfg, device="cuda:0")
     dp.create_diffusion_model()
     dp.create_pose_model()
-    dp.test_hyber(batches=list(synthetic_eval_batches(48, 16, seed=5)), is_train=1)
+    batches = list(synthetic_eval_batches(48, 16, seed=5))
+    p_fast = dp.test_hyber(batches=batches, is_train=1)
     assert len(dp.inference_times) == 3 and len(dp.memory_usage) == 3
     txt = (tmp_path / "performance_metrics.txt").read_text()
     assert txt.startswith("=== Performance Metrics ===\nTime (s): avg=")
     assert "Diffusion steps: 5\n" in txt and "Memory (MB): avg=" in txt and "=== Raw Data ===" in txt
+    assert "Pose model times: [" in txt and "Metrics times: [" in txt
+
+    slow_pose, slow_err = dp.model_pose.uvxyz, metrics.pose_errors
+
+    def pose_delayed(*a, **k):
+        time.sleep(0.25)
+        return slow_pose(*a, **k)
+
+    def errors_delayed(*a, **k):
+        time.sleep(0.25)
+        return slow_err(*a, **k)
+
+    dp.model_pose.uvxyz = pose_delayed
+    metrics.pose_errors = errors_delayed
+    try:
+        p_slow = dp.test_hyber(batches=batches, is_train=1)
+    finally:
+        metrics.pose_errors = slow_err
+        del dp.model_pose.uvxyz
+    assert p_slow == p_fast
+    assert min(dp.pose_times) >= 0.25 and min(dp.metrics_times) >= 0.25
+    assert max(dp.inference_times) < 0.2, dp.inference_times

@@ -159,3 +159,93 @@ def test_weights_reload_reaches_captured_graph(dev):
     assert torch.equal(out, ref2)
     del g
     m.close()
+
+
+def test_captured_eps_keeps_its_buffer(dev):
+    """advisor r02: a captured dpk_eps owns its projection buffer.  Capture eps at N on a stream,
+    then run an uncaptured eps at 2N on that same stream (which grows the stream's own buffer):
+    replays still give the eager result."""
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(256, seed=16)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    t = (torch.arange(128, device=dev, dtype=torch.float32) * 3) % 50
+    t2 = torch.full((256,), 11.0, device=dev)
+    eager = m(x[:128].contiguous(), mask, t, 0).clone()
+    eager2 = m(x, mask, t2, 0).clone()
+    s = torch.cuda.Stream(device=dev)
+    xin = x[:128].contiguous()
+    out = torch.empty_like(xin)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        out.copy_(m(xin, mask, t, 0))               # uncaptured call: sizes the spare
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        out.copy_(m(xin, mask, t, 0))
+    with torch.cuda.stream(s):                      # 2N uncaptured on the capture stream
+        big = m(x, mask, t2, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(big, eager2)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+    del g
+    m.close()
+
+
+def test_two_eps_graphs_replay_concurrently(dev):
+    """Two dpk_eps graphs captured on torch's (shared) capture stream with different timesteps,
+    replayed at the same time on two streams: each keeps its own projection buffer."""
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(512, seed=17)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    ta = torch.full((512,), 49.0, device=dev)
+    tb = torch.arange(512, device=dev, dtype=torch.float32) % 50
+    ra, rb = m(x, mask, ta, 0).clone(), m(x, mask, tb, 0).clone()
+    oa, ob = torch.empty_like(x), torch.empty_like(x)
+    graphs = []
+    for t, o in ((ta, oa), (tb, ob)):
+        o.copy_(m(x, mask, t, 0))                   # the uncaptured call before each capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            o.copy_(m(x, mask, t, 0))
+        graphs.append(g)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    for _ in range(4):
+        oa.zero_()
+        ob.zero_()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            graphs[0].replay()
+        with torch.cuda.stream(s2):
+            graphs[1].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(oa, ra) and torch.equal(ob, rb)
+    del graphs
+    m.close()
+
+
+def test_captured_eps_without_spare_is_refused(dev):
+    """Nothing is allocated inside a capture: a captured dpk_eps larger than the spare that the
+    uncaptured calls left fails with DPK_E_STATE (and the eager path still works after it)."""
+    from diffpose_amd._lib import DpkError
+
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(200, seed=18)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    t = torch.full((200,), 3.0, device=dev)
+    m(x[:64].contiguous(), mask, t[:64], 0)           # spare of 64 poses
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(DpkError) as ei:
+        with torch.cuda.graph(g):
+            m(x, mask, t, 0)
+    assert ei.value.code == -4
+    torch.cuda.synchronize()
+    ref = _model(dev)(x, mask, t, 0)
+    assert torch.equal(m(x, mask, t, 0), ref)
+    m.close()

@@ -4,13 +4,15 @@
     torch.manual_seed(0/1): xavier_normal_ Chebyshev weights, zero biases, identical attention
     projections, A_hat = I, models/ChebConv.py:62-67, models/gcndiff.py:70-98);
   * g10: the build's generator at a second seed (7).
-Goldens are the reference's own K=50 finals in fp32 and in fp64.  The tolerance is stated
-relative to the reference's own fp32-vs-fp64 gap on the same weights and inputs, g = |out32 -
-out64| (elementwise max) and gm = |MPJPE32 - MPJPE64| (mm):
-    elementwise  |hip - ref32| <= max(2e-5, 10 g)
-    MPJPE        |hip - ref32| <= max(1e-4 mm, 2 gm)
-(seed 1 of the reference init: gm = 2.8e-4 mm, above the north-star 1e-4 — the reference's own
-fp32 result is that uncertain there).  fp32 and the f16x3 GEMM mode are both held to these bars.
+Goldens are the reference's own K=50 finals in fp32 and in fp64; the reference's own fp32-vs-fp64
+gap on the same weights and inputs is g = |out32 - out64| (elementwise max) and gm = |MPJPE32 -
+MPJPE64| (mm).  Bars (verdict r02: set from what the kernel achieves, not from 10x the noise):
+    elementwise  |hip - ref32| <= ELEM_TOL = 5e-6 (the achieved deltas are printed and kept in
+                 profiles/r03_weight_ranges.txt; the old bar, max(2e-5, 10 g), was ~18x g)
+    MPJPE        |hip - ref32| <= 1e-4 mm (the north-star bar) on g9 seed 0 and g10;
+                 g9 seed 1 (gm = 2.8e-4 mm: the reference's own fp32 answer is that uncertain there)
+                 is reported against both 1e-4 mm and 2 gm and asserted against max(1e-4, 2 gm).
+fp32 and the f16x3 GEMM mode are both held to these bars.
 """
 import numpy as np
 import pytest
@@ -22,6 +24,7 @@ from diffpose_amd.weights import reference_init_state_dict, synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 
+ELEM_TOL = 5e-6
 CASES = ["g9_refinit_seed0.npz", "g9_refinit_seed1.npz", "g10_synth_seed7.npz"]
 
 
@@ -57,8 +60,16 @@ def test_sampler_on_other_weights(golden, name, gemm):
     ref, ref64 = g["out"].astype(np.float64), g["out64"]
     gap = float(np.abs(ref - ref64).max())
     gap_mm = abs(_mpjpe_mm(ref, g["targets"]) - _mpjpe_mm(ref64, g["targets"]))
-    assert np.abs(out - ref).max() <= max(2e-5, 10 * gap)
-    assert abs(_mpjpe_mm(out, g["targets"]) - _mpjpe_mm(ref, g["targets"])) <= max(1e-4, 2 * gap_mm)
+    d = float(np.abs(out - ref).max())
+    dm = abs(_mpjpe_mm(out, g["targets"]) - _mpjpe_mm(ref, g["targets"]))
+    de = float(np.abs(eps - g["eps"]).max())
+    seed1 = name == "g9_refinit_seed1.npz"
+    print(f"\nweight-range {name} {gemm}: eps max|d| {de:.3e}; K=50 final max|d| {d:.3e} (ref fp32-fp64 gap "
+          f"{gap:.3e}); MPJPE d {dm:.3e} mm (ref gap {gap_mm:.3e} mm) -> 1e-4 mm bar "
+          f"{'met' if dm <= 1e-4 else 'NOT met'}" + (f", 2*gap bar {2 * gap_mm:.3e} mm "
+                                                       f"{'met' if dm <= 2 * gap_mm else 'NOT met'}" if seed1 else ""))
+    assert d <= ELEM_TOL
+    assert dm <= (max(1e-4, 2 * gap_mm) if seed1 else 1e-4)
 
 
 def test_f16x3_range_guard():
