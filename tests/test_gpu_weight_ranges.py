@@ -9,9 +9,10 @@ gap on the same weights and inputs is g = |out32 - out64| (elementwise max) and 
 MPJPE64| (mm).  Bars (verdict r02: set from what the kernel achieves, not from 10x the noise):
     elementwise  |hip - ref32| <= ELEM_TOL = 5e-6 (the achieved deltas are printed and kept in
                  profiles/r03_weight_ranges.txt; the old bar, max(2e-5, 10 g), was ~18x g)
-    MPJPE        |hip - ref32| <= 1e-4 mm (the north-star bar) on g9 seed 0 and g10;
-                 g9 seed 1 (gm = 2.8e-4 mm: the reference's own fp32 answer is that uncertain there)
-                 is reported against both 1e-4 mm and 2 gm and asserted against max(1e-4, 2 gm).
+    MPJPE        |hip - ref32| <= 1e-4 mm (the north-star bar) on every case, g9 seed 1 included,
+                 although there the reference's own fp32-vs-fp64 gap (gm = 2.8e-4 mm) is above that
+                 bar; its line also reports the 2 gm bar the round-2 test used.
+Achieved on the MI355X (r03): final max|d| 6.0e-7 .. 9.0e-7, MPJPE d 2.9e-6 .. 1.9e-5 mm.
 fp32 and the f16x3 GEMM mode are both held to these bars.
 """
 import numpy as np
@@ -69,7 +70,7 @@ def test_sampler_on_other_weights(golden, name, gemm):
           f"{'met' if dm <= 1e-4 else 'NOT met'}" + (f", 2*gap bar {2 * gap_mm:.3e} mm "
                                                        f"{'met' if dm <= 2 * gap_mm else 'NOT met'}" if seed1 else ""))
     assert d <= ELEM_TOL
-    assert dm <= (max(1e-4, 2 * gap_mm) if seed1 else 1e-4)
+    assert dm <= 1e-4
 
 
 def test_f16x3_range_guard():

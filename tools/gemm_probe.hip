@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(NT, 1) probe(const float* W, float* out, long 
     __shared__ __attribute__((aligned(16))) float sm[SM_FLOATS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int i = tid; i < SM_FLOATS; i += NT) sm[i] = (i % 97) * 1e-3f;
+    for (int i = tid; i < SM_FLOATS; i += NT) sm[i] = ((i % 97) - 48) * 1e-2f;
     __syncthreads();
     float* A = sm + SM_B2;
     float* D = sm + SM_XS;
@@ -85,12 +85,24 @@ int main() {
     float* out;
     long long* cyc;
     hipMalloc(&W, 4 << 20);
-    hipMemset(W, 0, 4 << 20);
+    {   // nonzero weights (zero operands let the chip clock higher: MI355X_MICROARCH.md DVFS notes)
+        static float hw[1 << 20];
+        for (int i = 0; i < (1 << 20); ++i) hw[i] = ((i * 2654435761u) >> 8 & 0xffff) * (1.0f / 65536.0f) - 0.5f;
+        hipMemcpy(W, hw, 4 << 20, hipMemcpyHostToDevice);
+    }
     hipMalloc(&out, 256 * NT * 4);
     hipMalloc(&cyc, 256 * 8);
+#ifdef PROBE_SLOPE
+    // per-k-block slope and per-call intercept: each shape at KB and multiples (4x4x1 tails on)
+    run<18, 6, 2>("QKV", W, out, cyc); run<18, 12, 2>("QKV x2", W, out, cyc); run<18, 18, 2>("QKV x3", W, out, cyc);
+    run<12, 6, 2>("fc1", W, out, cyc); run<12, 12, 2>("fc1 x2", W, out, cyc);
+    run<6, 6, 2>("O", W, out, cyc); run<6, 12, 2>("fc2 / O x2", W, out, cyc); run<6, 18, 2>("C1/C2", W, out, cyc);
+    run<6, 36, 2>("C x2", W, out, cyc);
+#else
     for (int tm = 0; tm < 3; ++tm) {
         if (tm == 0) { run<18, 6, 0>("QKV", W, out, cyc); run<12, 6, 0>("fc1", W, out, cyc); run<6, 12, 0>("fc2", W, out, cyc); run<6, 18, 0>("C1/C2", W, out, cyc); run<6, 6, 0>("O", W, out, cyc); }
         if (tm == 2) { run<18, 6, 2>("QKV", W, out, cyc); run<12, 6, 2>("fc1", W, out, cyc); run<6, 12, 2>("fc2", W, out, cyc); run<6, 18, 2>("C1/C2", W, out, cyc); run<6, 6, 2>("O", W, out, cyc); }
     }
+#endif
     return 0;
 }
