@@ -30,11 +30,20 @@ __device__ __forceinline__ BPre<NCG> pre_tiles(const float* W, int ct0, int rot,
     return p;
 }
 
+// PROBE_MODE bit 1: no barriers; bit 2: no B prefetch (the ring's first blocks are zeros)
+#ifndef PROBE_MODE
+#define PROBE_MODE 0
+#endif
 template <int NCG, int NC, int KB>
 __device__ __forceinline__ void w8_gemm(const float* A, const float* W, const EpiArgs& e, int pr, int ct0, int lane) {
     const int rot = pr ? (NCG + 1) / 2 : 0;
-    const auto pre = pre_tiles<NCG, NC, KB>(W, ct0, rot, lane);
-    __syncthreads();
+    BPre<NCG> pre;
+    if constexpr (PROBE_MODE & 2) {
+        for (int c = 0; c < NCG; ++c) pre.b0[c] = pre.b1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        pre = pre_tiles<NCG, NC, KB>(W, ct0, rot, lane);
+    }
+    if constexpr (!(PROBE_MODE & 1)) __syncthreads();
     gemm_wave<2, NCG, TM_MFMA4, 0, NC, KB, E_STORE>(A, LD2, W, 2 * pr, ct0, rot, 64, (NCG & 1) && pr, lane, e, pre);
 }
 
@@ -61,7 +70,7 @@ __global__ void __launch_bounds__(64 * NW8, 1) probe(const float* W, float* out,
             if ((cg & 1) == 0) w8_gemm<NA, NC, KB>(A, W, e, pr, ct0, lane);
             else w8_gemm<NB, NC, KB>(A, W, e, pr, ct0, lane);
         }
-        __syncthreads();
+        if constexpr (!(PROBE_MODE & 1)) __syncthreads();
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
     if (tid == 0) cyc[blockIdx.x] = t1 - t0;
