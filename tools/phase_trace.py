@@ -17,7 +17,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO = os.path.join(ROOT, "build", "trace", "libdpk_trace.so")
+SO = os.environ.get("DPK_TRACE_SO", os.path.join(ROOT, "build", "trace", "libdpk_trace.so"))
 
 # stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
 # ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
