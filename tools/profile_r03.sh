@@ -1,4 +1,4 @@
-# Round-2 profiling recipe, run on a 1xMI355X gpurun box from the repo root:
+# Round-3 profiling recipe, run on a 1xMI355X gpurun box from the repo root:
 #   gpurun --timeout 1200 -- 'bash tools/profile_r03.sh r03_v15'
 # Writes gpurun_out/<tag>_*; the judged summaries are copied into profiles/ afterwards.
 # Every GPU step has its own time limit and the chain stops at the first failure.
