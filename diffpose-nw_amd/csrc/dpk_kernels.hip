@@ -88,6 +88,15 @@ struct SampleArgs {
     unsigned long long seed;
     int pose_off;         // first pose of this launch (a batch split over two launches, see launch_sampler)
     int num_layers;       // GraAttenLayer + _ResChebGC_diff pairs run (config num_layer, 1..NL)
+    // Step-split last round (sample mode, launch_sampler): the last split_n tiles run their K steps
+    // as two halves on two workgroups.  Blocks [0, split_n) run steps [0, split_k) of tiles
+    // split_full + b and publish x_t through x_out and flags[b]; blocks [split_n, split_n + split_full)
+    // run whole tiles; the last split_n blocks wait for their tile's flag and run [split_k, K).
+    int split_n;
+    int split_k;
+    int split_full;
+    unsigned* flags;      // [split_n] handoff words: 0 between launches, `token` once a first half is out
+    unsigned token;       // nonzero, per launch
 #if DPK_TRACE
     unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
     int trace_step;
@@ -207,7 +216,11 @@ struct dpk_handle {
     int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int n_cu = 256;                // compute units of the device (workgroups per round)
-    bool tail_split = true;        // balance the last round with 2-pose tiles (launch_sampler)
+    int tail_plan = 2;             // dpk_set_tail_plan: 0 4-pose tiles, 1 2-pose tail round, 2 step split
+    unsigned* flags = nullptr;     // device: FLAG_SLOTS x n_cu step-split handoff words (zero between launches)
+    std::vector<std::pair<hipStream_t, int>> flag_streams;   // flag slot of each stream (uncaptured calls)
+    int flag_used = 0;             // slots handed out (streams and captured calls)
+    unsigned token = 0;            // per-launch handoff token (never 0)
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
@@ -444,6 +457,22 @@ static int upload(dpk_handle* h) {
     return DPK_OK;
 }
 
+// Flag slot of a step-split launch on `st` (launch_sampler).  Uncaptured launches use one slot per
+// stream: launches on one stream run in order and each leaves its words at 0.  A captured launch
+// becomes a graph node that may replay on any stream, so it takes a slot of its own for good.
+// Null when every slot is taken (the caller then runs the 2-pose tail plan).
+constexpr int FLAG_SLOTS = 64;
+static unsigned* split_flags(dpk_handle* h, hipStream_t st, bool cap) {
+    if (!h->flags) return nullptr;
+    if (!cap)
+        for (auto& f : h->flag_streams)
+            if (f.first == st) return h->flags + (size_t)f.second * h->n_cu;
+    if (h->flag_used >= FLAG_SLOTS) return nullptr;
+    const int slot = h->flag_used++;
+    if (!cap) h->flag_streams.push_back({st, slot});
+    return h->flags + (size_t)slot * h->n_cu;
+}
+
 // One launch of the sampler kernel with tile size PT (4: dpk, 2: dpk2) for the handle's graph
 // pattern and GEMM mode.
 template <int MODE, int PT>
@@ -468,19 +497,42 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
 #undef DPK_LAUNCH
 }
 
-// The sampler over a.N poses.  One 4-pose workgroup per CU per round; when the last round would
-// leave at least half the CUs idle (at most 2 poses per CU remain) those poses run instead as
-// 2-pose workgroups (dpk2, about 0.6 of a 4-pose tile's time), one per CU, in a second launch
-// after the full rounds.  E.g. config 5's 2,560 poses per GPU: 2 full rounds + 256 2-pose tiles
-// instead of 2.5 rounds of 4-pose tiles (3 round times).  Each workgroup's result depends only on
-// its own poses, so the split changes no bits.
+// The sampler over a.N poses.  One 4-pose workgroup per CU per round; a partial last round of r
+// tiles would cost a whole round.  Plan 2 (sample mode, at least one full round before it,
+// r <= n_cu / 2): each of those tiles runs steps [0, K/2) and [K/2, K) on two workgroups, one
+// launch of full + 2r blocks ordered [first halves | full tiles | second halves].  The dispatcher
+// starts blocks in order as CUs free up, so the first halves run beside the first full round and
+// the second halves after the last one: the tail costs half a round, and a second half only ever
+// waits for a block numbered below it (no deadlock for any CU count).  E.g. config 5's 2,560
+// poses per GPU = 640 tiles: 2.5 round times instead of 3.  Every tile runs the same per-step
+// arithmetic, so the outputs are bitwise those of plan 0.
+// Plan 1 (and plan 2 where it does not apply): when the last round would leave at least half the
+// CUs idle (at most 2 poses per CU remain) those poses run as 2-pose workgroups (dpk2, about 0.6
+// of a 4-pose tile's time), one per CU, in a second launch after the full rounds.  Each
+// workgroup's result depends only on its own poses.
 template <int MODE>
-static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a) {
+static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap) {
     const int N = a.N;
     const int round4 = P * h->n_cu;
+    if constexpr (MODE == M_SAMPLE) {
+        const int tiles = (N + P - 1) / P, q = tiles / h->n_cu, r = tiles % h->n_cu;
+        if (h->tail_plan == 2 && a.K >= 2 && q >= 1 && r > 0 && 2 * r <= h->n_cu) {
+            if (unsigned* f = split_flags(h, st, cap)) {
+                a.pose_off = 0;
+                a.split_n = r;
+                a.split_k = a.K / 2;
+                a.split_full = q * h->n_cu;
+                a.flags = f;
+                if (++h->token == 0) ++h->token;
+                a.token = h->token;
+                launch_tiles<MODE, P>(h, q * h->n_cu + 2 * r, 0, st, a);
+                return;
+            }
+        }
+    }
     int n4 = N;
     const int rem = N % round4;
-    if (h->tail_split && rem != 0 && rem <= 2 * h->n_cu) n4 = N - rem;
+    if (h->tail_plan >= 1 && rem != 0 && rem <= 2 * h->n_cu) n4 = N - rem;
     if (n4 > 0) {
         a.pose_off = 0;
         launch_tiles<MODE, P>(h, (n4 + P - 1) / P, 0, st, a);
@@ -528,9 +580,15 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
         return DPK_E_HIP;
     }
     h->n_cu = std::max(h->n_cu, 1);
-    // DPK_TAIL_SPLIT=0: every round in 4-pose tiles (A/B timing); trace builds stamp per block id
-    if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_split = atoi(ts) != 0;
-    if (DPK_TRACE) h->tail_split = false;
+    // DPK_TAIL_SPLIT=0/1/2: the initial tail plan (A/B timing); trace builds stamp per block id
+    if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_plan = std::min(std::max(atoi(ts), 0), 2);
+    if (DPK_TRACE) h->tail_plan = 0;
+    if (hipMalloc(&h->flags, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess ||
+        hipMemset(h->flags, 0, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess) {
+        (void)hipStreamDestroy(h->aux);
+        delete h;
+        return DPK_E_HIP;
+    }
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_arena16.assign(ARENA16_BYTES / 2, 0);
     h->h_arenabf.assign(ARENA16_BYTES / 2, 0);
@@ -547,6 +605,7 @@ void dpk_destroy(dpk_handle* h) {
     if (h->arenabf) (void)hipFree(h->arenabf);
     if (h->temb) (void)hipFree(h->temb);
     if (h->tproj_zero) (void)hipFree(h->tproj_zero);
+    if (h->flags) (void)hipFree(h->flags);
     // hipFree waits for the device, so in-flight launches finish before their buffers go
     if (h->sched) sched_free(h->sched);
     for (Sched* s : h->retired) sched_free(s);
@@ -943,7 +1002,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
-    launch_sampler<M_EPS>(h, st, a);
+    launch_sampler<M_EPS>(h, st, a, cap);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
@@ -998,7 +1057,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    launch_sampler<M_SAMPLE>(h, st, a);
+    launch_sampler<M_SAMPLE>(h, st, a, cap);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return sched_note_use(h, sc, st, cap);
@@ -1034,7 +1093,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
-    launch_sampler<M_POSE>(h, st, a);
+    launch_sampler<M_POSE>(h, st, a, cap);
     HIPCHK(h, hipGetLastError());
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;
@@ -1045,6 +1104,13 @@ int dpk_set_gemm_mode(dpk_handle* h, int mode) {
     if (mode < 0 || mode > 2)
         return fail(h, DPK_E_INVALID, "dpk_set_gemm_mode: mode must be 0 (fp32), 1 (3xfp16) or 2 (bf16)");
     h->gemm_mode = mode;
+    return DPK_OK;
+}
+
+int dpk_set_tail_plan(dpk_handle* h, int plan) {
+    if (!h) return DPK_E_INVALID;
+    if (plan < 0 || plan > 2) return fail(h, DPK_E_INVALID, "dpk_set_tail_plan: plan must be 0, 1 or 2");
+    h->tail_plan = DPK_TRACE ? 0 : plan;
     return DPK_OK;
 }
 

@@ -17,7 +17,7 @@ ERRORS = {-1: "DPK_E_INVALID", -2: "DPK_E_UNSUPPORTED", -3: "DPK_E_HIP", -4: "DP
 
 # every symbol include/diffpose_kernels.h declares
 EXPORTS = ("dpk_version", "dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks", "dpk_set_schedule",
-           "dpk_eps", "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry", "dpk_last_error", "dpk_destroy")
+           "dpk_eps", "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_set_tail_plan", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry", "dpk_last_error", "dpk_destroy")
 
 
 class DpkConfig(ctypes.Structure):
@@ -62,6 +62,7 @@ def lib() -> ctypes.CDLL:
     L.dpk_gmm_sample.argtypes = [vp, vp, i32, i32, vp, i32, vp, u64, ctypes.c_double, vp, vp, vp, vp]
     L.dpk_gmm_sample_f64.argtypes = [vp, vp, i32, i32, vp, i32, vp, u64, ctypes.c_double, vp, vp, vp, vp]
     L.dpk_set_gemm_mode.argtypes = [vp, i32]
+    L.dpk_set_tail_plan.argtypes = [vp, i32]
     L.dpk_profile.argtypes = [vp, i32]
     L.dpk_profile_read.argtypes = [vp, fp, i32, ctypes.POINTER(i32)]
     L.dpk_kernel_geometry.argtypes = [ctypes.POINTER(i32)] * 3

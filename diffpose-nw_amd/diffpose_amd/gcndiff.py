@@ -198,6 +198,17 @@ class _HipModel:
         _lib.check(self._h, "dpk_set_gemm_mode", _lib.lib().dpk_set_gemm_mode(self._h, self.GEMM_MODES[mode]))
         self.gemm_mode = mode
 
+    TAIL_PLANS = {"four": 0, "two_pose": 1, "step_split": 2}
+
+    def set_tail_plan(self, plan: str = "step_split") -> None:
+        """How a partial last round of 4-pose tiles runs (see dpk_set_tail_plan): "step_split"
+        (default: its tiles' K steps split over two CUs, bitwise equal to "four"), "two_pose"
+        (a round of 2-pose tiles) or "four" (a round of 4-pose tiles).  Scheduling only: the
+        reference has no tiles."""
+        if plan not in self.TAIL_PLANS:
+            raise ValueError(f"tail plan must be one of {sorted(self.TAIL_PLANS)}, got {plan!r}")
+        _lib.check(self._h, "dpk_set_tail_plan", _lib.lib().dpk_set_tail_plan(self._h, self.TAIL_PLANS[plan]))
+
     def profile(self, enable: bool = True) -> None:
         """Bracket each model-kernel launch with HIP events (see dpk_profile)."""
         _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))

@@ -204,6 +204,22 @@ int dpk_gmm_sample_f64(const double* gmm_dev, const double* poses3d_dev, int n_s
  * shows as non-finite outputs. */
 int dpk_set_gemm_mode(dpk_handle* h, int mode);
 
+/* How dpk_sample balances a partial last round of tiles (4 poses per workgroup, one workgroup
+ * per CU per round; not part of the reference interface, which has no tiles):
+ *   plan 0: the last round in 4-pose tiles like the others;
+ *   plan 1: when it holds at most 2 poses per CU, one round of 2-pose tiles (about 0.6 of a
+ *           round);
+ *   plan 2 (default): when at least one full round precedes it and it holds at most half a
+ *           round of tiles, each of its tiles runs its K steps as two halves on two CUs (the
+ *           first half's x_t handed over through `out` and a device flag), so the last round
+ *           costs about half a round; otherwise plan 1.
+ * Plans 0 and 2 give bitwise the same outputs (the same tiles, the same per-step arithmetic);
+ * plan 1 agrees within fp32 rounding (other rows on the 4-row tail path).  Plan 2 needs a flag
+ * slot: one per caller stream for uncaptured calls and one per captured call, 64 per handle;
+ * a call that finds none left runs plan 1.  dpk_eps and dpk_pose (one step) use plan 1 for
+ * plan 2.  The environment variable DPK_TAIL_SPLIT sets the initial plan of a new handle. */
+int dpk_set_tail_plan(dpk_handle* h, int plan);
+
 /* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /
  * dpk_eps brackets its sampler-kernel launch with a pair of HIP events on the
  * caller's stream.  dpk_profile_read waits for the recorded events and returns up to

@@ -149,38 +149,59 @@ def test_large_batch_property(model, mask):
     assert torch.equal(big.view(20, 1024, 17, 5), base.unsqueeze(0).expand(20, -1, -1, -1))
 
 
-def test_tail_round_in_two_pose_tiles(model, mask):
-    """Config 5's per-GPU share (2,560 poses = 2.5 rounds of 4-pose workgroups on 256 CUs) runs as
-    2 full rounds of 4-pose tiles plus one round of 2-pose tiles (launch_sampler).  Each part is
-    bitwise the same as running its poses alone (the 2,048-pose head is 2 full rounds; the 512-pose
-    tail alone is one round of 2-pose tiles), the tail is within the fp32 bars of the oracle, and
-    a handle with the split disabled (DPK_TAIL_SPLIT=0: the tail as a half round of 4-pose tiles)
-    agrees within rounding (the tiles put different joints on the 4-row tail path)."""
-    import os
+def test_tail_round_plans(model, mask):
+    """Config 5's per-GPU share (2,560 poses = 640 4-pose tiles = 2.5 rounds on 256 CUs).
+    Plan "step_split" (default): the last 128 tiles run steps [0, 5) and [5, 10) on two CUs,
+    x_t handed over through the output buffer; bitwise equal to plan "four" (every tile in
+    4-pose tiles), trajectories and eta > 0 noise included.  Plan "two_pose": 2 full rounds + one
+    round of 2-pose tiles, each part bitwise what its poses give alone, within rounding of the
+    others (the tiles put different joints on the 4-row tail path).  Tail poses vs the oracle."""
     from oracle import gcndiff_oracle as O
 
     x, _ = synthetic_batch(2560, seed=23)
     xt = torch.from_numpy(x).cuda()
     seq = make_seq("uniform", 50, 10)
-    out = model.sample(xt, seq, _betas(51), mask=mask)
-    head = model.sample(xt[:2048].contiguous(), seq, _betas(51), mask=mask)
-    tail = model.sample(xt[2048:].contiguous(), seq, _betas(51), mask=mask)
-    assert torch.equal(out[:2048], head) and torch.equal(out[2048:], tail)
-    os.environ["DPK_TAIL_SPLIT"] = "0"
     try:
-        m4 = HipGCNdiff(adj_mx_from_edges(), None, device="cuda:0")
+        out = model.sample(xt, seq, _betas(51), mask=mask)
+        model.set_tail_plan("four")
+        out4 = model.sample(xt, seq, _betas(51), mask=mask)
+        assert torch.equal(out, out4)
+        xs4, x0s4 = model.sample(xt, seq, _betas(51), eta=0.5, seed=5, mask=mask, trajectory=True)
+        model.set_tail_plan("step_split")
+        xs2, x0s2 = model.sample(xt, seq, _betas(51), eta=0.5, seed=5, mask=mask, trajectory=True)
+        assert torch.equal(xs2, xs4) and torch.equal(x0s2, x0s4)
+        model.set_tail_plan("two_pose")
+        out1 = model.sample(xt, seq, _betas(51), mask=mask)
+        head = model.sample(xt[:2048].contiguous(), seq, _betas(51), mask=mask)
+        tail = model.sample(xt[2048:].contiguous(), seq, _betas(51), mask=mask)
+        assert torch.equal(out1[:2048], head) and torch.equal(out1[2048:], tail)
+        assert torch.equal(out4[:2048], head)
+        assert _maxdiff(out1, out) <= TRAJ_TOL
     finally:
-        del os.environ["DPK_TAIL_SPLIT"]
-    m4.load_state_dict(synthetic_state_dict())
-    out4 = m4.sample(xt, seq, _betas(51), mask=mask)
-    m4.close()
-    assert torch.equal(out4[:2048], head)
-    assert _maxdiff(out4, out) <= TRAJ_TOL
+        model.set_tail_plan("step_split")
     P, adj = O.params_to_torch(synthetic_state_dict()), O.adjacency()
     sel = torch.tensor([2048, 2049, 2050, 2051, 2558, 2559])
     xs, _ = O.generalized_steps(torch.from_numpy(x)[sel], torch.ones(1, 1, 17, dtype=torch.bool), seq,
                                 lambda a_, m_, t_: O.gcndiff_forward(P, adj, a_, m_, t_), _betas(51))
     assert _maxdiff(out[sel.cuda()], xs[-1]) <= TRAJ_TOL
+
+
+@pytest.mark.parametrize("n,k", [(1101, 25), (1100, 2), (2048 + 4 * 128, 50)])
+def test_step_split_matches_four_pose_plan(model, mask, n, k):
+    """Step split at other shapes: a ragged last tile (1,101 poses: 276 tiles, the last holding one
+    pose), an odd K (halves of 12 and 13 steps), K=2 (one step per half), and config 5's share at
+    K=50.  Bitwise equal to plan "four"; a repeated call (flags reset by every second half) too."""
+    x, _ = synthetic_batch(n, seed=29)
+    xt = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, k)
+    try:
+        model.set_tail_plan("four")
+        ref = model.sample(xt, seq, _betas(51), mask=mask)
+        model.set_tail_plan("step_split")
+        for _ in range(2):
+            assert torch.equal(model.sample(xt, seq, _betas(51), mask=mask), ref)
+    finally:
+        model.set_tail_plan("step_split")
 
 
 def test_eta_noise_statistics(model, mask):

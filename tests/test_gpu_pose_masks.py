@@ -167,10 +167,12 @@ def test_gcnpose_per_pose_masks_vs_oracle():
 @pytest.mark.parametrize("mode", ["eps", "sample"])
 def test_per_pose_masks_both_tile_sizes(model, mode):
     """N = 1,100 poses: one full round of 4-pose workgroups (poses 0..1023, the 4-pose kernel's
-    mask word wave / (NW/P) with pose_off 0) and a tail of 76 poses in 2-pose workgroups (the
-    second launch, pose_off 1024).  Four mask patterns in an irregular order: every pose equals
-    the same pose of the batch run with its pattern as the handle-wide mask, bitwise (same
-    launch geometry, only the mask's source differs)."""
+    mask word wave / (NW/P) with pose_off 0) and a tail of 76 poses, in 2-pose workgroups (eps
+    mode, and sample mode under the "two_pose" plan: the second launch, pose_off 1024) or, in
+    sample mode's default "step_split" plan, in 19 4-pose tiles whose steps run as two halves on
+    two workgroups (blocks numbered apart from their tiles).  Four mask patterns in an irregular
+    order: every pose equals the same pose of the batch run with its pattern as the handle-wide
+    mask, bitwise (same launch geometry, only the mask's source differs)."""
     n = 1100
     x, _ = synthetic_batch(n, seed=26)
     x = torch.from_numpy(x).cuda()
@@ -188,11 +190,16 @@ def test_per_pose_masks_both_tile_sizes(model, mode):
             return model(x, mask, t, 0)
         return model.sample(x, seq, _betas(51), mask=mask)
 
-    out = run(per)
-    for k in range(4):
-        ref = run(pats[k : k + 1].cuda())
-        sel = (which == k).nonzero().flatten().cuda()
-        assert torch.equal(out[sel], ref[sel]), (mode, k)
+    for plan in (["step_split", "two_pose"] if mode == "sample" else ["step_split"]):
+        model.set_tail_plan(plan)
+        try:
+            out = run(per)
+            for k in range(4):
+                ref = run(pats[k : k + 1].cuda())
+                sel = (which == k).nonzero().flatten().cuda()
+                assert torch.equal(out[sel], ref[sel]), (mode, plan, k)
+        finally:
+            model.set_tail_plan("step_split")
     head = (which[:1024] == 2).nonzero().flatten()
     tail = 1024 + (which[1024:] == 2).nonzero().flatten()
     assert head.numel() > 0 and tail.numel() > 0   # the key-16-alone pattern lands in both tile sizes

@@ -65,6 +65,89 @@ def test_graph_capture_replays_bitwise(dev):
     m.close()
 
 
+def _capture(dev, m, x, seq, out):
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        m.sample(x, seq, _betas(), out=out)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.sample(x, seq, _betas(), out=out)
+    return g
+
+
+def test_graph_capture_step_split_replays_bitwise(dev):
+    """2,560 poses (config 5's per-GPU share): the captured launch runs the step-split last round
+    on a flag slot of its own; every replay leaves the flags at 0 for the next, and eager calls
+    on the capture stream in between (their own slot) do not disturb it."""
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(2560, seed=14)[0]).to(dev)
+    seq = make_seq("uniform", 50, 10)
+    eager = m.sample(x, seq, _betas()).clone()
+    m.set_tail_plan("four")
+    assert torch.equal(m.sample(x, seq, _betas()), eager)
+    m.set_tail_plan("step_split")
+    out = torch.empty_like(x)
+    g = _capture(dev, m, x, seq, out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        assert torch.equal(m.sample(x, seq, _betas()), eager)
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+    del g
+    m.close()
+
+
+def test_step_split_on_three_streams_without_sync(dev):
+    """Step-split launches (1,100 poses, 3 schedules) on three streams at once: one flag slot per
+    stream, results equal to the sequential ones."""
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(1100, seed=15)[0]).to(dev)
+    seqs = [make_seq("uniform", 50, 50), make_seq("uniform", 50, 10), make_seq("uniform", 50, 25)]
+    ref = [_model(dev).sample(x, q, _betas()).clone() for q in seqs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in seqs]
+    outs = [torch.empty_like(x) for _ in seqs]
+    for _ in range(2):
+        for st, q, o in zip(streams, seqs, outs):
+            st.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(st):
+                m.sample(x, q, _betas(), out=o)
+        torch.cuda.synchronize()
+        for o, r in zip(outs, ref):
+            assert torch.equal(o, r)
+    m.close()
+
+
+def test_flag_slots_exhausted_fall_back_to_two_pose_tiles(dev):
+    """A handle has 64 flag slots; captured step-split launches keep theirs for good.  Once they
+    are gone a capture runs the 2-pose tail plan instead (bitwise that plan's eager result), and
+    the graphs captured earlier still replay the step-split result."""
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(1100, seed=16)[0]).to(dev)
+    seq = make_seq("uniform", 50, 2)
+    ref2 = m.sample(x, seq, _betas()).clone()
+    m.set_tail_plan("two_pose")
+    ref1 = m.sample(x, seq, _betas()).clone()
+    m.set_tail_plan("step_split")
+    assert not torch.equal(ref1, ref2)
+    outs, graphs = [], []
+    for _ in range(66):
+        outs.append(torch.empty_like(x))
+        graphs.append(_capture(dev, m, x, seq, outs[-1]))
+    for g, o in zip(graphs, outs):
+        o.zero_()
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], ref2)
+    assert torch.equal(outs[-1], ref1)
+    del graphs
+    m.close()
+
+
 def test_set_schedule_after_capture_keeps_graph_and_eager_correct(dev):
     m = _model(dev)
     x = torch.from_numpy(synthetic_batch(64, seed=12)[0]).to(dev)
