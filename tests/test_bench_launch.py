@@ -62,3 +62,19 @@ def test_bench_config4_eight_ranks_cpu_dry():
     assert len(line["per_rank_ms"]) == 8
     assert line["reassembly_ok"] is True
     assert line["allgather_ms"] > 0
+
+
+def test_bench_config5_eight_ranks_cpu_dry():
+    """BASELINE config 5 at 8 GPUs (1,024 frames x H=20, strong scaling): 8 ranks, 128 frames x 20
+    hypotheses = 2,560 rows each (the share the step-split last round runs on the GPU), reassembled
+    through the all-gather on rank 0 (gloo here; RCCL on the node)."""
+    rc, line, err = _run(["--gpus", "8", "--config", "5", "--cpu-dry", "--steps", "2", "--warmup", "1"],
+                         timeout=420)
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 8
+    assert line["scaling"] == "strong"
+    assert line["config"]["baseline_config"] == 5
+    assert line["config"]["frames_total"] == 1024 and line["config"]["frames_per_gpu"] == 128
+    assert line["config"]["rows_per_gpu"] == 2560
+    assert len(line["per_rank_ms"]) == 8
+    assert line["reassembly_ok"] is True
