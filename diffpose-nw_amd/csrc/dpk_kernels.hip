@@ -211,8 +211,12 @@ struct EpsBuf {
     int cap = 0;
 };
 
+struct GenModel;   // dpk_generic.inc: the forward for model shapes other than the compiled one
+
 struct dpk_handle {
     int device = 0;
+    GenModel* gen = nullptr;       // non-null: this handle's shape runs on the generic path
+    int n_pts = J;                 // joints of the handle's model
     int kind = 0;                  // 0: GCNdiff (coords 5->5), 1: GCNpose (coords 2->3)
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int n_cu = 256;                // compute units of the device (workgroups per round)
@@ -547,6 +551,8 @@ static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap
     }
 }
 
+#include "dpk_generic.inc"
+
 extern "C" {
 
 int dpk_version(void) { return 100; }
@@ -561,11 +567,18 @@ int dpk_kernel_geometry(int* ppw, int* tpw, int* lds) {
 int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (!cfg || !out) return DPK_E_INVALID;
     *out = nullptr;
-    if (cfg->hid_dim != D || cfg->num_layers < 1 || cfg->num_layers > NL || cfg->n_head != NH || cfg->n_pts != J)
+    // the compiled shape runs the persistent sampler; any other (hid_dim a multiple of n_head,
+    // n_pts <= 32, any num_layer) the generic path (dpk_generic.inc); DPK_FORCE_GENERIC=1 sends the
+    // compiled shape there too (tests compare the two)
+    const char* fg = getenv("DPK_FORCE_GENERIC");
+    const bool compiled = cfg->hid_dim == D && cfg->num_layers >= 1 && cfg->num_layers <= NL && cfg->n_head == NH &&
+                          cfg->n_pts == J && !(fg && atoi(fg) != 0);
+    if (cfg->hid_dim < 2 || cfg->n_head < 1 || cfg->hid_dim % cfg->n_head != 0 || cfg->num_layers < 1 ||
+        cfg->n_pts < 2 || cfg->n_pts > dpkg::GJ_MAX || cfg->coords_in < 1 || cfg->coords_out < 1)
         return DPK_E_UNSUPPORTED;
     int kind;
-    if (cfg->coords_in == CIN && cfg->coords_out == COUT) kind = 0;
-    else if (cfg->coords_in == CIN_POSE && cfg->coords_out == COUT_POSE) kind = 1;
+    if (cfg->coords_in == CIN_POSE && cfg->coords_out == COUT_POSE) kind = 1;
+    else if (compiled ? (cfg->coords_in == CIN && cfg->coords_out == COUT) : cfg->coords_in == cfg->coords_out) kind = 0;
     else return DPK_E_UNSUPPORTED;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return DPK_E_HIP;
@@ -573,6 +586,9 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     h->device = cfg->device;
     h->kind = kind;
     h->num_layers = cfg->num_layers;
+    h->n_pts = cfg->n_pts;
+    if (!compiled)
+        h->gen = gen_new(cfg->hid_dim, cfg->n_head, cfg->n_pts, cfg->num_layers, cfg->coords_in, cfg->coords_out, kind);
     if (hipSetDevice(h->device) != hipSuccess ||
         hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) {
@@ -606,6 +622,7 @@ void dpk_destroy(dpk_handle* h) {
     if (h->temb) (void)hipFree(h->temb);
     if (h->tproj_zero) (void)hipFree(h->tproj_zero);
     if (h->flags) (void)hipFree(h->flags);
+    gen_free(h->gen);
     // hipFree waits for the device, so in-flight launches finish before their buffers go
     if (h->sched) sched_free(h->sched);
     for (Sched* s : h->retired) sched_free(s);
@@ -626,6 +643,11 @@ const char* dpk_last_error(const dpk_handle* h) { return h ? h->err.c_str() : "n
 
 int dpk_set_graph(dpk_handle* h, const float* adj) {
     if (!h || !adj) return fail(h, DPK_E_INVALID, "dpk_set_graph: null argument");
+    if (h->gen) {
+        gen_set_graph(h->gen, adj);
+        h->have_graph = true;
+        return h->have_weights ? gen_upload(h, h->gen) : DPK_OK;
+    }
     float T1[J * J], T2[J * J];
     cheb_terms(adj, T1, T2);
     for (int i = 0; i < J * J; ++i) {
@@ -656,7 +678,7 @@ int dpk_set_graph(dpk_handle* h, const float* adj) {
 int dpk_set_mask(dpk_handle* h, const uint8_t* m) {
     if (!h || !m) return fail(h, DPK_E_INVALID, "dpk_set_mask: null argument");
     unsigned bits = 0;
-    for (int j = 0; j < J; ++j)
+    for (int j = 0; j < h->n_pts; ++j)
         if (m[j]) bits |= 1u << j;
     h->mask = bits;
     return DPK_OK;
@@ -701,6 +723,11 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         }
         return it->second.first;
     };
+    if (h->gen) {
+        if (!gen_load(h->gen, get)) return fail(h, DPK_E_WEIGHTS, "dpk_load_weights: " + missing);
+        h->have_weights = true;
+        return gen_upload(h, h->gen);
+    }
 #define GET(var, key, numel)                                             \
     const float* var = get(key, numel);                                  \
     if (!var) return fail(h, DPK_E_WEIGHTS, "dpk_load_weights: " + missing);
@@ -910,7 +937,7 @@ int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* s
         sched_free(s);
         return fail(h, DPK_E_HIP, std::string("dpk_set_schedule: coef upload: ") + hipGetErrorString(e));
     }
-    if (h->have_weights) {
+    if (h->have_weights && !h->gen) {   // the generic path computes its projections per call
         const int rc = sched_compute_tps(h, s);
         if (rc) {
             sched_free(s);
@@ -930,6 +957,9 @@ static int check_ready(dpk_handle* h, int kind = 0) {
                                          : "GCNpose handle (coords 2->3): use dpk_pose");
     if (!h->have_graph) return fail(h, DPK_E_STATE, "graph (adjacency) not set");
     if (!h->have_weights) return fail(h, DPK_E_STATE, "weights not loaded");
+    if (h->gen && h->gemm_mode != 0)
+        return fail(h, DPK_E_UNSUPPORTED, "generic-shape path (model shape other than hid 96 / 4 heads / 17 joints): "
+                                          "fp32 GEMMs only (gemm mode 0)");
     if (h->gemm_mode == 1 && !h->w16_ok)
         return fail(h, DPK_E_UNSUPPORTED, "gemm mode 1 (3x fp16): a GEMM weight has |w| >= 1015, outside the split-fp16 "
                                           "packing range; use gemm mode 0 (fp32)");
@@ -948,6 +978,7 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     bool cap = false;
     rc = capturing(h, st, &cap);
     if (rc) return rc;
+    if (h->gen) return gen_eps(h, x, t, eps, N, st, cap);
     float* proj = nullptr;
     if (cap) {
         // a graph node keeps this buffer: take the spare (sized by earlier uncaptured calls) for good
@@ -1017,7 +1048,8 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     Sched* sc = h->sched;
     if (!sc) return fail(h, DPK_E_STATE, "schedule not set");
     if (N == 0) return DPK_OK;
-    if (sc->tps_gen != h->weights_gen) return fail(h, DPK_E_STATE, "dpk_sample: schedule projections are stale");
+    if (!h->gen && sc->tps_gen != h->weights_gen)
+        return fail(h, DPK_E_STATE, "dpk_sample: schedule projections are stale");
     if ((rc = check_pose_masks(h, N, "dpk_sample"))) return rc;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
@@ -1025,6 +1057,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     rc = capturing(h, st, &cap);
     if (rc) return rc;
     if (!cap) sched_sweep(h);
+    if (h->gen) return gen_sample(h, sc, x, out, xs, x0s, N, seed, st, cap);
     if (xs) HIPCHK(h, hipMemcpyAsync(xs, x, (size_t)N * PE * 4, hipMemcpyDeviceToDevice, st));
     SampleArgs a{};
     a.arena = h->arena;
@@ -1077,6 +1110,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     bool cap = false;
     rc = capturing(h, st, &cap);
     if (rc) return rc;
+    if (h->gen) return gen_pose(h, x2d, xyz, uvxyz, N, H, root_mode, st, cap);
     SampleArgs a{};
     a.arena = h->arena;
     a.num_layers = h->num_layers;

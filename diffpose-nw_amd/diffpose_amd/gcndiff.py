@@ -72,6 +72,9 @@ class _HipModel:
         self._h = h
         self.n_pts = npts
         self.num_layer = nl
+        self.hid_dim = hid
+        self.n_head = nh
+        self.coords_dim = tuple(coords)
         adj = adj.detach().cpu().numpy() if torch.is_tensor(adj) else np.asarray(adj)
         self.adj = np.ascontiguousarray(adj, dtype=np.float32)
         if self.adj.shape != (npts, npts):
@@ -87,7 +90,8 @@ class _HipModel:
     # -- nn.Module-like surface -------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True):
         """Accept the reference's states[0] (with/without 'module.'), torch tensors or numpy."""
-        sd = normalize_state_dict(state_dict, kind=self.KIND, n_layers=self.num_layer)
+        sd = normalize_state_dict(state_dict, kind=self.KIND, n_layers=self.num_layer, hid=self.hid_dim,
+                                  n_pts=self.n_pts, coords=self.coords_dim)
         names = list(sd.keys())
         arrs = [np.ascontiguousarray(sd[k], dtype=np.float32) for k in names]
         c_names = (ctypes.c_char_p * len(names))(*[k.encode() for k in names])
@@ -177,7 +181,8 @@ class _HipModel:
             self._mask_key = key
             self._mask_ref = mask
 
-    def _check_x(self, x, channels: int = 5):
+    def _check_x(self, x, channels: int | None = None):
+        channels = self.coords_dim[0] if channels is None else channels
         if not (torch.is_tensor(x) and x.is_cuda and x.dtype == torch.float32):
             raise TypeError("x must be a float32 CUDA(HIP) tensor")
         if x.dim() != 3 or x.shape[1] != self.n_pts or x.shape[2] != channels:

@@ -147,14 +147,15 @@ def strip_module_prefix(sd) -> "OrderedDict[str, object]":
     return out
 
 
-def normalize_state_dict(sd, kind: str = "diff", n_layers: int = N_LAYERS) -> "OrderedDict[str, np.ndarray]":
+def normalize_state_dict(sd, kind: str = "diff", n_layers: int = N_LAYERS, hid: int = HID, n_pts: int = N_PTS,
+                         coords=None) -> "OrderedDict[str, np.ndarray]":
     """Validate a GCNdiff (GCNpose) state_dict against the layout; return float32 numpy arrays.
 
     Raises KeyError for missing/unexpected keys and ValueError for shape
     mismatches, mirroring ``nn.Module.load_state_dict(strict=True)``.
     """
     sd = strip_module_prefix(sd)
-    shapes = param_shapes(kind=kind, n_layers=n_layers)
+    shapes = param_shapes(kind=kind, n_layers=n_layers, hid=hid, n_pts=n_pts, coords=coords)
     missing = [k for k in shapes if k not in sd]
     unexpected = [k for k in sd if k not in shapes]
     if missing or unexpected:

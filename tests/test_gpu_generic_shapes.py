@@ -1,0 +1,152 @@
+"""GPU: GCNdiff / GCNpose at model shapes other than the compiled one (hid_dim 96, n_head 4,
+n_pts 17), which run on the generic-shape path (csrc/dpk_generic.inc).  The reference builds its
+models from any config (models/gcndiff.py:55-99, models/gcnpose.py:55-98); every config it ships
+uses the compiled shape (configs/human36m_*.yml:9-16), so there are no reference golden vectors at
+these shapes: the checker is the oracle, which issues the reference's ATen ops for any hid_dim,
+n_head and n_pts and is pinned bit-exact to the reference's goldens at the shipped shape
+(tests/test_oracle_golden.py) — parity here is pinned through the oracle, not by fixtures.
+
+Tolerances as tests/test_gpu_parity.py: 2e-5 elementwise for eps and trajectories (fp32 sums in
+another order), MPJPE-style bars are not used (no targets at these shapes).
+"""
+import os
+from types import SimpleNamespace as ns
+
+import numpy as np
+import pytest
+import torch
+
+from diffpose_amd.data import synthetic_batch
+from diffpose_amd.gcndiff import H36M_EDGES, HipGCNdiff, adj_mx_from_edges
+from diffpose_amd.schedule import get_beta_schedule, make_seq
+from diffpose_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+CHAIN16 = tuple((i, i + 1) for i in range(15))
+
+
+def _betas(T=51):
+    return torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
+                                              num_diffusion_timesteps=T)).float()
+
+
+def _cfg(hid, heads, layers, npts, coords=(5, 5)):
+    return ns(model=ns(hid_dim=hid, emd_dim=hid, coords_dim=list(coords), num_layer=layers, n_head=heads,
+                       dropout=0.25, n_pts=npts))
+
+
+def _maxdiff(a, b):
+    return float((a.detach().cpu().double() - b.detach().cpu().double()).abs().max())
+
+
+def _inputs(n, npts, seed):
+    x, _ = synthetic_batch(n, seed=seed)
+    x = torch.from_numpy(x)
+    if npts != 17:
+        x = x[:, :npts].contiguous()
+    return x
+
+
+SHAPES = [
+    (64, 2, 2, 17, H36M_EDGES),     # narrower, fewer heads and layers, the H36M skeleton
+    (128, 8, 3, 17, H36M_EDGES),    # wider, more heads
+    (48, 4, 1, 16, CHAIN16),        # another skeleton: a 16-joint chain
+]
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("hid,heads,layers,npts,edges", SHAPES)
+def test_generic_eps_and_sample_vs_oracle(dev, hid, heads, layers, npts, edges):
+    from oracle import gcndiff_oracle as O
+
+    sd = synthetic_state_dict(hid=hid, n_layers=layers, n_pts=npts)
+    adj = adj_mx_from_edges(npts, edges)
+    m = HipGCNdiff(adj, _cfg(hid, heads, layers, npts), device=dev)
+    m.load_state_dict(sd)
+    P = O.params_to_torch(sd)
+    g = torch.from_numpy(adj)
+    fwd = lambda a, mk, t: O.gcndiff_forward(P, g, a, mk, t, n_layers=layers, heads=heads)  # noqa: E731
+    x = _inputs(24, npts, seed=40 + hid)
+    t = torch.arange(24, dtype=torch.float32) * 2.0
+    ones = torch.ones(1, 1, npts, dtype=torch.bool)
+    eps = m(x.to(dev), ones.to(dev), t.to(dev), 0)
+    ref = fwd(x, ones, t)
+    assert eps.shape == ref.shape and _maxdiff(eps, ref) <= TOL
+    # a handle-wide key mask and per-pose masks (the reference's masked_fill broadcast)
+    mk = ones.clone()
+    mk[0, 0, [0, npts - 1]] = False
+    assert _maxdiff(m(x.to(dev), mk.to(dev), t.to(dev), 0), fwd(x, mk, t)) <= TOL
+    per = torch.ones(24, 1, npts, dtype=torch.bool)
+    per[::3, 0, 1::2] = False
+    per[1::5, 0, :npts - 1] = False
+    assert _maxdiff(m(x.to(dev), per.to(dev), t.to(dev), 0), fwd(x, per, t)) <= TOL
+    # the K=10 sampler with its trajectory
+    seq = make_seq("uniform", 50, 10)
+    xs, x0s = m.sample(x.to(dev), seq, _betas(), mask=ones.to(dev), trajectory=True)
+    rxs, rx0s = O.generalized_steps(x, ones, seq, fwd, _betas())
+    assert _maxdiff(xs, torch.stack(rxs)) <= TOL and _maxdiff(x0s, torch.stack(rx0s)) <= TOL
+    out = m.sample(x.to(dev), seq, _betas(), mask=ones.to(dev))
+    assert torch.equal(out, xs[-1])
+    m.close()
+
+
+def test_generic_path_matches_fused_at_the_compiled_shape(dev):
+    """DPK_FORCE_GENERIC=1 puts the compiled shape on the generic path: it agrees with the fused
+    sampler within the fp32 bars (different summation orders), on 64 poses at K=50."""
+    x = _inputs(64, 17, seed=50).to(dev)
+    seq = make_seq("uniform", 50, 50)
+    fused = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
+    fused.load_state_dict(synthetic_state_dict())
+    os.environ["DPK_FORCE_GENERIC"] = "1"
+    try:
+        gen = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
+    finally:
+        del os.environ["DPK_FORCE_GENERIC"]
+    gen.load_state_dict(synthetic_state_dict())
+    a = fused.sample(x, seq, _betas())
+    b = gen.sample(x, seq, _betas())
+    assert _maxdiff(a, b) <= TOL
+    with pytest.raises(RuntimeError):
+        gen.set_gemm_mode("f16x3")
+        gen.sample(x, seq, _betas())
+    fused.close()
+    gen.close()
+
+
+def test_generic_gcnpose_vs_oracle(dev):
+    from diffpose_amd.gcnpose import HipGCNpose
+    from oracle import gcndiff_oracle as O
+
+    hid, heads, layers = 64, 2, 2
+    sd = synthetic_state_dict(kind="pose", hid=hid, n_layers=layers)
+    m = HipGCNpose(adj_mx_from_edges(), _cfg(hid, heads, layers, 17, coords=(2, 3)), device=dev)
+    m.load_state_dict(sd)
+    x2d = _inputs(20, 17, seed=60)[:, :, :2].contiguous()
+    ones = torch.ones(1, 1, 17, dtype=torch.bool)
+    xyz = m(x2d.to(dev), ones.to(dev))
+    ref = O.gcnpose_forward(O.params_to_torch(sd), O.adjacency(), x2d, ones, n_layers=layers, heads=heads)
+    assert _maxdiff(xyz, ref) <= TOL
+    uv = m.uvxyz(x2d.to(dev), ones.to(dev), test_times=3, root_mode="quirk")
+    assert _maxdiff(uv, O.build_uvxyz(x2d, ref, 3, "quirk")) <= TOL
+    m.close()
+
+
+def test_generic_path_refuses_capture(dev):
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(64, 2, 1, 17), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=64, n_layers=1))
+    x = _inputs(8, 17, seed=70).to(dev)
+    seq = make_seq("uniform", 50, 2)
+    m.sample(x, seq, _betas())
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(Exception):
+        with torch.cuda.graph(g):
+            m.sample(x, seq, _betas())
+    m.close()
