@@ -571,14 +571,17 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     // n_pts <= 32, any num_layer) the generic path (dpk_generic.inc); DPK_FORCE_GENERIC=1 sends the
     // compiled shape there too (tests compare the two)
     const char* fg = getenv("DPK_FORCE_GENERIC");
+    const bool pose_io = cfg->coords_in == CIN_POSE && cfg->coords_out == COUT_POSE;
     const bool compiled = cfg->hid_dim == D && cfg->num_layers >= 1 && cfg->num_layers <= NL && cfg->n_head == NH &&
-                          cfg->n_pts == J && !(fg && atoi(fg) != 0);
+                          cfg->n_pts == J && (pose_io || (cfg->coords_in == CIN && cfg->coords_out == COUT)) &&
+                          !(fg && atoi(fg) != 0);
     if (cfg->hid_dim < 2 || cfg->n_head < 1 || cfg->hid_dim % cfg->n_head != 0 || cfg->num_layers < 1 ||
         cfg->n_pts < 2 || cfg->n_pts > dpkg::GJ_MAX || cfg->coords_in < 1 || cfg->coords_out < 1)
         return DPK_E_UNSUPPORTED;
+    // GCNpose: coords 2 -> 3; GCNdiff: x and eps share a shape (coords in == out)
     int kind;
-    if (cfg->coords_in == CIN_POSE && cfg->coords_out == COUT_POSE) kind = 1;
-    else if (compiled ? (cfg->coords_in == CIN && cfg->coords_out == COUT) : cfg->coords_in == cfg->coords_out) kind = 0;
+    if (pose_io) kind = 1;
+    else if (cfg->coords_in == cfg->coords_out) kind = 0;
     else return DPK_E_UNSUPPORTED;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) return DPK_E_HIP;

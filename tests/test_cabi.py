@@ -47,17 +47,24 @@ def test_argument_validation_without_gpu():
     L = _lib.lib()
     h = ctypes.c_void_p()
     assert L.dpk_create(None, ctypes.byref(h)) == -1
-    bad = _lib.DpkConfig(128, 5, 4, 17, 5, 5, 0)            # hid_dim other than the compiled 96
-    assert L.dpk_create(ctypes.byref(bad), ctypes.byref(h)) == -2
+    # shapes outside what either path runs are refused before any device call (DPK_E_UNSUPPORTED);
+    # other shapes than the compiled one (hid 96, 4 heads, 17 joints) pass to the generic path and
+    # only then need a device (none here: DPK_E_HIP)
+    for cfg, rc in (((100, 5, 8, 17, 5, 5), -2),      # hid_dim not a multiple of n_head
+                    ((96, 5, 4, 40, 5, 5), -2),       # more than 32 joints (one mask word per pose)
+                    ((96, 5, 4, 17, 3, 4), -2),       # GCNdiff needs coords in == out (or GCNpose's 2 -> 3)
+                    ((128, 5, 4, 17, 5, 5), -3),      # generic path: another hid_dim
+                    ((96, 5, 4, 17, 3, 3), -3)):      # generic path: other coords
+        c = _lib.DpkConfig(*cfg, 0)
+        assert L.dpk_create(ctypes.byref(c), ctypes.byref(h)) == rc, cfg
     assert L.dpk_eps(None, None, None, None, 0, None) == -1
     assert L.dpk_last_error(None) == b"null handle"
-    bad_pose = _lib.DpkConfig(96, 5, 4, 17, 3, 3, 0)        # coords other than [5,5] / [2,3]
-    assert L.dpk_create(ctypes.byref(bad_pose), ctypes.byref(h)) == -2
     assert L.dpk_pose(None, None, None, None, 0, 1, 0, None) == -1
     assert L.dpk_set_pose_masks(None, None, 0) == -1
-    # num_layers is a run-time value in 1..5 (config num_layer); 0 and 6 are rejected before any
-    # device call, 3 passes the shape check and only then needs a device (none here: DPK_E_HIP)
-    for nl, rc in ((0, -2), (6, -2), (3, -3)):
+    # num_layers is a run-time value (config num_layer): 1..5 on the compiled sampler, more on the
+    # generic path; 0 is rejected before any device call, 3 and 6 pass the shape check and only then
+    # need a device (none here: DPK_E_HIP)
+    for nl, rc in ((0, -2), (6, -3), (3, -3)):
         cfg = _lib.DpkConfig(96, nl, 4, 17, 5, 5, 0)
         assert L.dpk_create(ctypes.byref(cfg), ctypes.byref(h)) == rc, nl
     # metrics entry validates before launching: negative F, H < 1, unknown root mode, null outputs
