@@ -74,7 +74,13 @@ typedef struct {
 int dpk_version(void);
 
 /* Create a handle on cfg->device.  Replaces GCNdiff(adj, config) construction
- * (models/gcndiff.py:55-99; runners/diffpose_frame.py:118-127). */
+ * (models/gcndiff.py:55-99; runners/diffpose_frame.py:118-127).  The shape every reference config
+ * uses (hid_dim 96, n_head 4, n_pts 17, num_layer 1..5, coords [5,5] or GCNpose's [2,3]) runs the
+ * persistent sampler; any other shape with hid_dim a multiple of n_head, n_pts <= 32 and coords
+ * in == out (or [2,3]) runs the generic-shape path: the same model as per-op HIP kernels, fp32 GEMMs
+ * only (dpk_set_gemm_mode 1/2 then fail with DPK_E_UNSUPPORTED), no graph capture (a captured call
+ * fails with DPK_E_UNSUPPORTED), per-stream scratch grown on demand.  Other shapes:
+ * DPK_E_UNSUPPORTED. */
 int dpk_create(const dpk_config* cfg, dpk_handle** out);
 
 /* Dense n_pts x n_pts adjacency as passed to GCNdiff(adj, ...) (row-normalised,
