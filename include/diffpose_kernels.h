@@ -47,7 +47,7 @@ extern "C" {
 
 #define DPK_OK              0
 #define DPK_E_INVALID      -1   /* bad argument (null pointer, N<0, size mismatch)       */
-#define DPK_E_UNSUPPORTED  -2   /* model dims other than the compiled GCNdiff shape      */
+#define DPK_E_UNSUPPORTED  -2   /* model dims / mode neither path supports               */
 #define DPK_E_HIP          -3   /* HIP runtime error                                     */
 #define DPK_E_STATE        -4   /* weights / graph / schedule not set yet                */
 #define DPK_E_WEIGHTS      -5   /* unknown, missing or mis-sized state_dict entry        */
@@ -55,11 +55,11 @@ extern "C" {
 typedef struct dpk_handle dpk_handle;
 
 /* Model hyper-parameters (configs/human36m_diffpose_uvxyz_*.yml model: section,
- * emd_dim = 4*hid_dim per models/gcndiff.py:68).  The kernels are compiled for
+ * emd_dim = 4*hid_dim per models/gcndiff.py:68).  The persistent sampler is compiled for
  * hid_dim 96, n_head 4, n_pts 17 and coords_dim [5,5] (GCNdiff, the denoiser) or [2,3]
- * (GCNpose, the 2D->3D front-end; runners/diffpose_frame.py:138); num_layers (the
- * config's num_layer, models/gcndiff.py:63-90) is a run-time value in 1..5 (the
- * reference's configs all use 5).  Other values: DPK_E_UNSUPPORTED. */
+ * (GCNpose, the 2D->3D front-end; runners/diffpose_frame.py:138), with num_layers (the
+ * config's num_layer, models/gcndiff.py:63-90) a run-time value in 1..5 (the reference's
+ * configs all use 5); other shapes run the generic-shape path (dpk_create). */
 typedef struct {
     int hid_dim;
     int num_layers;
