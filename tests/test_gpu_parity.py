@@ -186,11 +186,13 @@ def test_tail_round_plans(model, mask):
     assert _maxdiff(out[sel.cuda()], xs[-1]) <= TRAJ_TOL
 
 
-@pytest.mark.parametrize("n,k", [(1101, 25), (1100, 2), (2048 + 4 * 128, 50)])
+@pytest.mark.parametrize("n,k", [(1101, 25), (1100, 2), (2048 + 4 * 128, 50), (1025, 10), (1536, 10),
+                                 (2048 + 4 * 128 + 3, 10)])
 def test_step_split_matches_four_pose_plan(model, mask, n, k):
     """Step split at other shapes: a ragged last tile (1,101 poses: 276 tiles, the last holding one
-    pose), an odd K (halves of 12 and 13 steps), K=2 (one step per half), and config 5's share at
-    K=50.  Bitwise equal to plan "four"; a repeated call (flags reset by every second half) too."""
+    pose), an odd K (halves of 12 and 13 steps), K=2 (one step per half), config 5's share at K=50,
+    a single split tile holding one pose (1,025), half a round (1,536) and a ragged 2.5 rounds.
+    Bitwise equal to plan "four"; a repeated call (flags reset by every second half) too."""
     x, _ = synthetic_batch(n, seed=29)
     xt = torch.from_numpy(x).cuda()
     seq = make_seq("uniform", 50, k)
