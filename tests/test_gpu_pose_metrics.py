@@ -89,7 +89,9 @@ def test_handle_kinds_are_enforced(pose_model):
     x2d = torch.zeros(4, 17, 2, device="cuda:0")
     with pytest.raises(DpkError):
         HipGCNpose._launch(d, x2d, None, None, torch.empty(4, 17, 5, device="cuda:0"), 1, "quirk")
-    with pytest.raises(DpkError):
+    with pytest.raises(DpkError):      # input shaped for the pose handle: the library refuses the kind
+        HipGCNdiff.forward(pose_model, torch.zeros(4, 17, 2, device="cuda:0"), None, torch.zeros(4, device="cuda:0"))
+    with pytest.raises(ValueError):    # uvxyz-shaped input: refused by the shape check first
         HipGCNdiff.forward(pose_model, torch.zeros(4, 17, 5, device="cuda:0"), None, torch.zeros(4, device="cuda:0"))
     with pytest.raises(ValueError):
         pose_model(torch.zeros(4, 17, 5, device="cuda:0"), None)
