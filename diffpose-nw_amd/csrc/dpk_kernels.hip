@@ -595,6 +595,8 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (hipSetDevice(h->device) != hipSuccess ||
         hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) {
+        if (h->aux) (void)hipStreamDestroy(h->aux);
+        gen_free(h->gen);
         delete h;
         return DPK_E_HIP;
     }
@@ -604,7 +606,9 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     if (DPK_TRACE) h->tail_plan = 0;
     if (hipMalloc(&h->flags, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess ||
         hipMemset(h->flags, 0, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess) {
+        if (h->flags) (void)hipFree(h->flags);
         (void)hipStreamDestroy(h->aux);
+        gen_free(h->gen);
         delete h;
         return DPK_E_HIP;
     }

@@ -221,8 +221,10 @@ int dpk_set_gemm_mode(dpk_handle* h, int mode);
  *           costs about half a round; otherwise plan 1.
  * Plans 0 and 2 give bitwise the same outputs (the same tiles, the same per-step arithmetic);
  * plan 1 agrees within fp32 rounding (other rows on the 4-row tail path).  Plan 2 needs a flag
- * slot: one per caller stream for uncaptured calls and one per captured call, 64 per handle;
- * a call that finds none left runs plan 1.  dpk_eps and dpk_pose (one step) use plan 1 for
+ * slot: one per caller stream for uncaptured calls and one per captured call, 64 per handle,
+ * never released before dpk_destroy (a caller cycling through many short-lived streams uses
+ * them up); a call that finds none left runs plan 1.  A second half waits for its first half
+ * at most ~8 s (a first half that never arrives: that tile's output is NaN, not a hang).  dpk_eps and dpk_pose (one step) use plan 1 for
  * plan 2.  The environment variable DPK_TAIL_SPLIT sets the initial plan of a new handle. */
 int dpk_set_tail_plan(dpk_handle* h, int plan);
 
