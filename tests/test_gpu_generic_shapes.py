@@ -114,6 +114,12 @@ def test_generic_path_matches_fused_at_the_compiled_shape(dev):
     a = fused.sample(x, seq, _betas())
     b = gen.sample(x, seq, _betas())
     assert _maxdiff(a, b) <= TOL
+    # eta > 0: both paths draw the same counter-based noise, keyed by (seed, step, element)
+    seq10 = make_seq("uniform", 50, 10)
+    a = fused.sample(x, seq10, _betas(), eta=0.5, seed=7)
+    b = gen.sample(x, seq10, _betas(), eta=0.5, seed=7)
+    assert _maxdiff(a, b) <= TOL
+    assert _maxdiff(a, fused.sample(x, seq10, _betas(), eta=0.5, seed=8)) > 1e-3
     with pytest.raises(RuntimeError):
         gen.set_gemm_mode("f16x3")
         gen.sample(x, seq, _betas())

@@ -206,6 +206,21 @@ def test_step_split_matches_four_pose_plan(model, mask, n, k):
         model.set_tail_plan("step_split")
 
 
+def test_step_split_quad_schedule(model, mask):
+    """The step split under the quad skip (duplicate t values, runners/diffpose_frame.py:314-317)
+    with eta > 0: bitwise equal to plan "four" (the schedule and the noise keys are per step)."""
+    x, _ = synthetic_batch(1536, seed=31)
+    xt = torch.from_numpy(x).cuda()
+    seq = make_seq("quad", 50, 20)
+    try:
+        model.set_tail_plan("four")
+        ref = model.sample(xt, seq, _betas(51), eta=0.3, seed=11, mask=mask)
+        model.set_tail_plan("step_split")
+        assert torch.equal(model.sample(xt, seq, _betas(51), eta=0.3, seed=11, mask=mask), ref)
+    finally:
+        model.set_tail_plan("step_split")
+
+
 def test_eta_noise_statistics(model, mask):
     """eta > 0 draws N(0,1) noise in-kernel (counter-based; not torch.randn_like): check
     determinism per seed and the moments of the recovered noise (parity is statistical)."""
