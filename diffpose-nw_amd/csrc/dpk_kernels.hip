@@ -675,6 +675,19 @@ int dpk_set_graph(dpk_handle* h, const float* adj) {
         for (int k = 0; k < SPAT.n2[i]; ++k)
             h->h_arena[OFF_CHEBS + SPAT.nnz1 + SPAT.o2[i] + k] = T2[i * J + SPAT.c2[i][k]];
     }
+    // padded rows of the same values for the output ChebConv (OFF_CHEBT): (value bits, row offset j'*LD2)
+    for (int i = 0; i < J; ++i) {
+        float* row = &h->h_arena[OFF_CHEBT + (size_t)i * (SPT1 + SPT2) * 2];
+        for (int k = 0; k < SPT1 + SPT2; ++k) {
+            const bool t1 = k < SPT1;
+            const int kk = t1 ? k : k - SPT1;
+            const int n = t1 ? SPAT.n1[i] : SPAT.n2[i];
+            const int col = kk < n ? (t1 ? SPAT.c1[i][kk] : SPAT.c2[i][kk]) : i;
+            row[2 * k] = kk < n ? (t1 ? T1 : T2)[i * J + col] : 0.f;
+            const int32_t off = col * LD2;
+            memcpy(&row[2 * k + 1], &off, 4);
+        }
+    }
     h->sparse_graph = fits;
     h->h_adj.assign(adj, adj + J * J);
     h->have_graph = true;
