@@ -27,6 +27,8 @@ Also reported on the same JSON line:
                 N=1 only), best of --cpu-repeats after a warm-up call, at the host threads the
                 job is allotted (OMP_NUM_THREADS; --cpu-threads adds legs);
   parity        MPJPE (mm) of the HIP result vs the oracle on those frames, and max |diff|;
+  mpjpe         the job's MPJPE / P-MPJPE over all frames by the final reduction: per-frame errors on
+                every rank (dpk_pose_metrics) and one all-gather of 16 B per frame (after the timed steps);
   variants      the same measurement (warmup, timed steps, roofline, parity) in the other GEMM
                 modes: the headline is fp32 MFMA (the reference's arithmetic); "f16x3" runs the
                 layer GEMMs as three fp16-split MFMA products with fp32 accumulation; "bf16"
@@ -421,6 +423,35 @@ def rank_main(args):
             ok = torch.tensor([1 if torch.equal(full[idx], out) else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             reassembly = bool(ok.item())
+    # ---- the final MPJPE reduction (runners/diffpose_frame.py:382-387): per-frame (MPJPE, P-MPJPE) of this
+    #      rank's frames (dpk_pose_metrics: hypothesis mean, root-relative, Procrustes, fp64), then one
+    #      all-gather of those 16 B per frame; every rank ends with the job's MPJPE.  Once, after the timed steps.
+    tg_local = torch.from_numpy(tgt_all[lo:hi]).to(dev)
+    if use_dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    if dry:    # no HIP metrics kernel on CPU: MPJPE of the stub output, P-MPJPE not computed
+        o = out.double().view(args.hyp, hi - lo, 17, 5).mean(0)[:, :, 2:]
+        fe = torch.stack([torch.norm(o - o[:, :1] - tg_local.double(), dim=-1).mean(-1),
+                          torch.full((hi - lo,), float("nan"), dtype=torch.float64)], dim=1)
+    else:
+        from diffpose_amd.metrics import pose_errors
+
+        fe = torch.stack(pose_errors(out, tg_local, args.hyp, root_mode="relative"), dim=1)
+    if use_dist:
+        fe = D.gather_frames(fe, B_total, 1)
+    sync()
+    reduce_s = time.perf_counter() - t0
+    if use_dist:
+        reduce_s = D.max_over_ranks(reduce_s, device=dev)
+    fe_h = fe.cpu().numpy()
+    mpjpe_line = {"p1_mm": round(float(fe_h[:, 0].mean()) * 1000.0, 6),
+                  "p2_mm": None if dry else round(float(fe_h[:, 1].mean()) * 1000.0, 6),
+                  "frames": int(fe_h.shape[0]), "reduce_ms": round(reduce_s * 1e3, 4),
+                  "how": ("per-frame (MPJPE, P-MPJPE) on each rank's frames (dpk_pose_metrics, fp64), " +
+                          ("one RCCL all_gather of 16 B per frame" if use_dist else "one rank, no collective")),
+                  "targets": "synthetic (seeded), root-relative"}
     out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0 and not dry) else None
     variants = {}
     if args.variants and not dry:
@@ -469,6 +500,7 @@ def rank_main(args):
         result.update({"dtype": "fp32", "data": "cpu-dry rehearsal: elementwise stub instead of the sampler",
                        "value": None, "roofline": None})
         result["config"]["parallelism"] = f"dp{world} frame-sharded + gloo all_gather (cpu-dry)"
+    result["mpjpe"] = mpjpe_line
     if allgather_ms is not None:
         result["allgather_ms"] = round(allgather_ms, 4)
         result["reassembly_ok"] = reassembly

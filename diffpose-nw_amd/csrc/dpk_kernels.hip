@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -86,6 +88,7 @@ struct SampleArgs {
     const unsigned* pmask;  // per-pose 17-bit key masks [N] (dpk_set_pose_masks), or null: `mask` for all
     float eta;
     unsigned long long seed;
+    const float* noise;   // [K][N][17][5] caller noise for c1*z (the reference's per-step randn_like), or null: Philox
     int pose_off;         // first pose of this launch (a batch split over two launches, see launch_sampler)
     int num_layers;       // GraAttenLayer + _ResChebGC_diff pairs run (config num_layer, 1..NL)
     // Step-split last round (sample mode, launch_sampler): the last split_n tiles run their K steps
@@ -95,8 +98,10 @@ struct SampleArgs {
     int split_n;
     int split_k;
     int split_full;
-    unsigned* flags;      // [split_n] handoff words: 0 between launches, `token` once a first half is out
-    unsigned token;       // nonzero, per launch
+    unsigned* flags;      // [split_n] handoff words: 0 between launches, (token << 2) | state during one
+    unsigned token;       // nonzero, per launch (30 bits)
+    int* split_stats;     // device counter: second halves that recomputed their first half's steps
+    int split_dbg;        // dpk_debug_split: 0 normal; 1 first halves start late; 2 no idle wait
 #if DPK_TRACE
     unsigned long long* trace;   // [blocks][NW][TRACE_SLOTS]
     int trace_step;
@@ -159,14 +164,15 @@ __global__ void __launch_bounds__(256) temb_kernel(const float* __restrict__ tw,
     }
 }
 
-// Elementwise DDIM update for externally computed eps.
+// Elementwise DDIM update for externally computed eps; z from the caller's draws of this step
+// (`noise`, n floats) or counter-based.
 __global__ void __launch_bounds__(256) ddim_kernel(const float* __restrict__ xt, const float* __restrict__ et,
                                                    float* __restrict__ xn, float* __restrict__ x0o, long long n,
                                                    const float* __restrict__ cf, int step, float eta,
-                                                   unsigned long long seed) {
+                                                   unsigned long long seed, const float* __restrict__ noise) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    const float z = eta != 0.f ? normal_noise(seed, step, i) : 0.f;
+    const float z = noise ? noise[i] : (eta != 0.f ? normal_noise(seed, step, i) : 0.f);
     float x0, x1;
     ddim_elem(cf, xt[i], et[i], z, x0, x1);
     xn[i] = x1;
@@ -194,7 +200,7 @@ struct Sched {
     float eta = 0.f;
     std::vector<float> h_coef;
     uint64_t tps_gen = 0;          // weights generation tps was computed from (0: not yet)
-    bool pinned = false;           // read by a captured graph: kept until dpk_destroy
+    int pins = 0;                  // captured graphs that read it (CapRes): kept while any is alive
     std::vector<std::pair<hipStream_t, hipEvent_t>> uses;   // last launch on each stream
 };
 
@@ -211,6 +217,28 @@ struct EpsBuf {
     int cap = 0;
 };
 
+// What the launches captured in one stream capture (one hipGraph) read by address: the schedules
+// they were captured with, dpk_eps projection buffers (one per capturing stream: the captured
+// launches of one stream are sequential graph nodes and share it) and step-split flag slots (one
+// per capturing stream likewise).  A HIP user object retained by the capture's graph drops the
+// graph's reference when the graph and its executable instances are destroyed (host callback, no
+// HIP calls); the handle's next uncaptured call then waits for the device once and recycles the
+// resources.  Where the runtime cannot retain one, they are kept until dpk_destroy.
+struct CapRes {
+    unsigned long long id = 0;                 // capture sequence id (hipStreamGetCaptureInfo_v2)
+    std::atomic<int> refs{1};                  // the handle's reference (+1 while a graph holds one)
+    std::atomic<bool> released{false};
+    bool tracked = false;                      // a graph retains our user object
+    std::vector<Sched*> scheds;
+    std::vector<EpsBuf> eps;                   // per capturing stream
+    std::vector<std::pair<hipStream_t, int>> slots;   // flag slot per capturing stream
+};
+static void cap_release_cb(void* p) {
+    CapRes* c = static_cast<CapRes*>(p);
+    c->released.store(true);
+    if (c->refs.fetch_sub(1) == 1) delete c;
+}
+
 struct GenModel;   // dpk_generic.inc: the forward for model shapes other than the compiled one
 
 struct dpk_handle {
@@ -221,10 +249,14 @@ struct dpk_handle {
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int n_cu = 256;                // compute units of the device (workgroups per round)
     int tail_plan = 2;             // dpk_set_tail_plan: 0 4-pose tiles, 1 2-pose tail round, 2 step split
-    unsigned* flags = nullptr;     // device: FLAG_SLOTS x n_cu step-split handoff words (zero between launches)
-    std::vector<std::pair<hipStream_t, int>> flag_streams;   // flag slot of each stream (uncaptured calls)
-    int flag_used = 0;             // slots handed out (streams and captured calls)
-    unsigned token = 0;            // per-launch handoff token (never 0)
+    unsigned* flags = nullptr;     // device: FLAG_SLOTS x n_cu step-split handoff words (zero between launches),
+                                   // then the split fallback counter
+    std::vector<int> slot_free;    // flag slots no launch holds
+    std::vector<std::pair<int, hipEvent_t>> slot_busy;   // uncaptured launches: slot until its event completes
+    std::vector<hipEvent_t> slot_ev;   // idle events for slot_busy
+    int split_dbg = 0;             // dpk_debug_split mode
+    unsigned token = 0;            // per-launch handoff token (30 bits, never 0)
+    std::vector<CapRes*> caps;     // resources of captured launches (per capture)
     std::string err;
     float* arena = nullptr;        // device: packed weights + graph constants
     float* temb = nullptr;         // device: timestep-MLP weights
@@ -234,8 +266,7 @@ struct dpk_handle {
     Sched* sched = nullptr;        // current schedule
     std::vector<Sched*> retired;   // replaced schedules not yet known to be unused
     std::vector<EpsBuf> eps_bufs;  // per stream (uncaptured dpk_eps)
-    EpsBuf eps_spare;              // unused buffer for the next captured dpk_eps (no stream)
-    std::vector<float*> eps_pinned;   // buffers owned by captured dpk_eps launches (freed at destroy)
+    EpsBuf eps_spare;              // unused buffer for the next capture's dpk_eps (no stream)
     std::vector<float> h_arena;    // host staging of the arena
     char* arena16 = nullptr;       // device: split-fp16 GEMM weights (gemm mode 1)
     std::vector<uint16_t> h_arena16;
@@ -392,11 +423,11 @@ static void sched_free(Sched* s) {
     delete s;
 }
 
-// Free the retired schedules whose every recorded use has completed (never the pinned ones).
+// Free the retired schedules whose every recorded use has completed (never one a live graph reads).
 static void sched_sweep(dpk_handle* h) {
     std::vector<Sched*> keep;
     for (Sched* s : h->retired) {
-        bool done = !s->pinned;
+        bool done = s->pins == 0;
         for (auto& u : s->uses) done = done && hipEventQuery(u.second) == hipSuccess;
         if (done) sched_free(s);
         else keep.push_back(s);
@@ -404,11 +435,85 @@ static void sched_sweep(dpk_handle* h) {
     h->retired.swap(keep);
 }
 
-// After enqueuing a launch that reads `s` on `st`: pin it if the launch was captured, else
-// record its completion on that stream.
+// The CapRes of the capture `st` is recording into (created on its first captured launch).
+static int cap_get(dpk_handle* h, hipStream_t st, CapRes** out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    HIPCHK(h, hipStreamGetCaptureInfo_v2(st, &cs, &id, &graph, nullptr, nullptr));
+    for (CapRes* c : h->caps)
+        if (c->id == id) {
+            *out = c;
+            return DPK_OK;
+        }
+    CapRes* c = new CapRes();
+    c->id = id;
+    // DPK_CAPTURE_RELEASE=1: hand the graph a user object that releases the resources with it
+    const char* env = getenv("DPK_CAPTURE_RELEASE");
+    if (graph && env && atoi(env) == 1) {
+        c->refs.fetch_add(1);              // the graph's reference (dropped by cap_release_cb)
+        hipUserObject_t obj = nullptr;
+        if (hipUserObjectCreate(&obj, c, cap_release_cb, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+            c->refs.fetch_sub(1);
+            (void)hipGetLastError();
+        } else if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipUserObjectRelease(obj, 1);   // runs the callback: drops the graph's reference
+        } else {
+            c->tracked = true;
+        }
+    }
+    h->caps.push_back(c);
+    *out = c;
+    return DPK_OK;
+}
+
+static void slot_put(dpk_handle* h, int slot) { h->slot_free.push_back(slot); }
+
+// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  The release
+// callback may run while a replay is still in flight on some stream, so the device is drained once
+// before anything is reused (graph destruction is rare; nothing waits otherwise).
+static void cap_sweep(dpk_handle* h) {
+    bool any = false;
+    for (CapRes* c : h->caps) any = any || (c->tracked && c->released.load());
+    if (!any) return;
+    if (hipDeviceSynchronize() != hipSuccess) {    // e.g. another thread is capturing: try again later
+        (void)hipGetLastError();
+        return;
+    }
+    std::vector<CapRes*> keep;
+    for (CapRes* c : h->caps) {
+        if (!(c->tracked && c->released.load())) {
+            keep.push_back(c);
+            continue;
+        }
+        for (Sched* s : c->scheds) --s->pins;
+        for (auto& e : c->eps) {
+            if (!h->eps_spare.p || h->eps_spare.cap < e.cap) {
+                if (h->eps_spare.p) (void)hipFree(h->eps_spare.p);
+                h->eps_spare = EpsBuf{nullptr, e.p, e.cap};
+            } else {
+                (void)hipFree(e.p);
+            }
+        }
+        for (auto& s : c->slots) slot_put(h, s.second);
+        if (c->refs.fetch_sub(1) == 1) delete c;
+    }
+    h->caps.swap(keep);
+    sched_sweep(h);
+}
+
+// After enqueuing a launch that reads `s` on `st`: pin it to the capture if the launch was
+// captured, else record its completion on that stream.
 static int sched_note_use(dpk_handle* h, Sched* s, hipStream_t st, bool cap) {
     if (cap) {
-        s->pinned = true;
+        CapRes* c = nullptr;
+        const int rc = cap_get(h, st, &c);
+        if (rc) return rc;
+        if (std::find(c->scheds.begin(), c->scheds.end(), s) == c->scheds.end()) {
+            c->scheds.push_back(s);
+            ++s->pins;
+        }
         return DPK_OK;
     }
     hipEvent_t ev = nullptr;
@@ -461,20 +566,55 @@ static int upload(dpk_handle* h) {
     return DPK_OK;
 }
 
-// Flag slot of a step-split launch on `st` (launch_sampler).  Uncaptured launches use one slot per
-// stream: launches on one stream run in order and each leaves its words at 0.  A captured launch
-// becomes a graph node that may replay on any stream, so it takes a slot of its own for good.
-// Null when every slot is taken (the caller then runs the 2-pose tail plan).
+// Flag slots of step-split launches (launch_sampler).  No two launches that may overlap share a slot:
+// an uncaptured launch holds one until an event recorded behind it has completed (checked at the
+// next launch), a captured one for the life of its graph (shared by the captured launches of one
+// stream, which are sequential graph nodes; every launch leaves its words at 0).  -1 when all are
+// held (the caller then runs the 2-pose tail plan).
 constexpr int FLAG_SLOTS = 64;
-static unsigned* split_flags(dpk_handle* h, hipStream_t st, bool cap) {
-    if (!h->flags) return nullptr;
-    if (!cap)
-        for (auto& f : h->flag_streams)
-            if (f.first == st) return h->flags + (size_t)f.second * h->n_cu;
-    if (h->flag_used >= FLAG_SLOTS) return nullptr;
-    const int slot = h->flag_used++;
-    if (!cap) h->flag_streams.push_back({st, slot});
-    return h->flags + (size_t)slot * h->n_cu;
+static int split_slot(dpk_handle* h, hipStream_t st, bool cap) {
+    if (!h->flags) return -1;
+    if (cap) {
+        CapRes* c = nullptr;
+        if (cap_get(h, st, &c)) return -1;
+        for (auto& s : c->slots)
+            if (s.first == st) return s.second;
+        if (h->slot_free.empty()) return -1;
+        const int slot = h->slot_free.back();
+        h->slot_free.pop_back();
+        c->slots.push_back({st, slot});
+        return slot;
+    }
+    std::vector<std::pair<int, hipEvent_t>> busy;
+    for (auto& b : h->slot_busy) {
+        if (hipEventQuery(b.second) == hipSuccess) {
+            h->slot_free.push_back(b.first);
+            h->slot_ev.push_back(b.second);
+        } else {
+            busy.push_back(b);
+        }
+    }
+    (void)hipGetLastError();          // hipEventQuery's hipErrorNotReady
+    h->slot_busy.swap(busy);
+    if (h->slot_free.empty()) return -1;
+    const int slot = h->slot_free.back();
+    h->slot_free.pop_back();
+    return slot;
+}
+// after an uncaptured launch that used `slot` on `st`
+static int split_slot_hold(dpk_handle* h, int slot, hipStream_t st) {
+    hipEvent_t ev = nullptr;
+    if (!h->slot_ev.empty()) {
+        ev = h->slot_ev.back();
+        h->slot_ev.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        h->slot_free.push_back(slot);    // the launch is enqueued; a later launch reusing the slot is
+        HIPCHK(h, hipStreamSynchronize(st));   // safe once this one has finished
+        return DPK_OK;
+    }
+    h->slot_busy.push_back({slot, ev});
+    HIPCHK(h, hipEventRecord(ev, st));
+    return DPK_OK;
 }
 
 // One launch of the sampler kernel with tile size PT (4: dpk, 2: dpk2) for the handle's graph
@@ -515,22 +655,27 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
 // of a 4-pose tile's time), one per CU, in a second launch after the full rounds.  Each
 // workgroup's result depends only on its own poses.
 template <int MODE>
-static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap) {
+static int launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap) {
     const int N = a.N;
     const int round4 = P * h->n_cu;
     if constexpr (MODE == M_SAMPLE) {
         const int tiles = (N + P - 1) / P, q = tiles / h->n_cu, r = tiles % h->n_cu;
         if (h->tail_plan == 2 && a.K >= 2 && q >= 1 && r > 0 && 2 * r <= h->n_cu) {
-            if (unsigned* f = split_flags(h, st, cap)) {
+            const int slot = split_slot(h, st, cap);
+            if (slot >= 0) {
                 a.pose_off = 0;
                 a.split_n = r;
                 a.split_k = a.K / 2;
                 a.split_full = q * h->n_cu;
-                a.flags = f;
-                if (++h->token == 0) ++h->token;
+                a.flags = h->flags + (size_t)slot * h->n_cu;
+                a.split_stats = reinterpret_cast<int*>(h->flags + (size_t)FLAG_SLOTS * h->n_cu);
+                a.split_dbg = h->split_dbg;
+                h->token = (h->token + 1) & 0x3fffffffu;
+                if (h->token == 0) h->token = 1;
                 a.token = h->token;
                 launch_tiles<MODE, P>(h, q * h->n_cu + 2 * r, 0, st, a);
-                return;
+                HIPCHK(h, hipGetLastError());
+                return cap ? DPK_OK : split_slot_hold(h, slot, st);
             }
         }
     }
@@ -549,6 +694,8 @@ static void launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap
         a.pose_off = n4;
         launch_tiles<MODE, P2>(h, (N - n4 + P2 - 1) / P2, pad, st, a);
     }
+    HIPCHK(h, hipGetLastError());
+    return DPK_OK;
 }
 
 #include "dpk_generic.inc"
@@ -590,6 +737,7 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     h->kind = kind;
     h->num_layers = cfg->num_layers;
     h->n_pts = cfg->n_pts;
+    h->mask = cfg->n_pts >= 32 ? ~0u : (1u << cfg->n_pts) - 1u;   // every key attends (all-ones src_mask)
     if (!compiled)
         h->gen = gen_new(cfg->hid_dim, cfg->n_head, cfg->n_pts, cfg->num_layers, cfg->coords_in, cfg->coords_out, kind);
     if (hipSetDevice(h->device) != hipSuccess ||
@@ -604,8 +752,10 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     // DPK_TAIL_SPLIT=0/1/2: the initial tail plan (A/B timing); trace builds stamp per block id
     if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_plan = std::min(std::max(atoi(ts), 0), 2);
     if (DPK_TRACE) h->tail_plan = 0;
-    if (hipMalloc(&h->flags, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess ||
-        hipMemset(h->flags, 0, (size_t)FLAG_SLOTS * h->n_cu * 4) != hipSuccess) {
+    // FLAG_SLOTS x n_cu handoff words + the fallback counter
+    const size_t flag_bytes = ((size_t)FLAG_SLOTS * h->n_cu + 4) * 4;
+    for (int s = FLAG_SLOTS - 1; s >= 0; --s) h->slot_free.push_back(s);
+    if (hipMalloc(&h->flags, flag_bytes) != hipSuccess || hipMemset(h->flags, 0, flag_bytes) != hipSuccess) {
         if (h->flags) (void)hipFree(h->flags);
         (void)hipStreamDestroy(h->aux);
         gen_free(h->gen);
@@ -636,7 +786,13 @@ void dpk_destroy(dpk_handle* h) {
     for (auto& b : h->eps_bufs)
         if (b.p) (void)hipFree(b.p);
     if (h->eps_spare.p) (void)hipFree(h->eps_spare.p);
-    for (float* p : h->eps_pinned) (void)hipFree(p);
+    for (CapRes* c : h->caps) {
+        for (auto& e : c->eps) (void)hipFree(e.p);
+        // a graph still alive keeps the CapRes object (its callback touches only that)
+        if (c->refs.fetch_sub(1) == 1) delete c;
+    }
+    for (auto& b : h->slot_busy) (void)hipEventDestroy(b.second);
+    for (hipEvent_t e : h->slot_ev) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     for (auto* v : {&h->ev_used, &h->ev_free})
         for (auto& e : *v) {
@@ -1001,15 +1157,30 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     if (h->gen) return gen_eps(h, x, t, eps, N, st, cap);
     float* proj = nullptr;
     if (cap) {
-        // a graph node keeps this buffer: take the spare (sized by earlier uncaptured calls) for good
-        if (h->eps_spare.cap < N)
-            return fail(h, DPK_E_STATE, "dpk_eps: a captured call needs a projection buffer of " + std::to_string(N) +
-                                            " poses, and the spare holds " + std::to_string(h->eps_spare.cap) +
-                                            "; make an uncaptured dpk_eps call of >= N poses before each capture");
-        proj = h->eps_spare.p;
-        h->eps_pinned.push_back(proj);
-        h->eps_spare = EpsBuf{};
+        // graph nodes keep this buffer: the capture's own for this stream (its captured dpk_eps calls
+        // are sequential nodes and share it), taken from the spare that uncaptured calls size
+        CapRes* c = nullptr;
+        if ((rc = cap_get(h, st, &c))) return rc;
+        EpsBuf* mine = nullptr;
+        for (auto& e : c->eps)
+            if (e.st == st) mine = &e;
+        if (!mine) {
+            if (h->eps_spare.cap < N)
+                return fail(h, DPK_E_STATE, "dpk_eps: a captured call needs a projection buffer of " +
+                                                std::to_string(N) + " poses, and the spare holds " +
+                                                std::to_string(h->eps_spare.cap) +
+                                                "; make an uncaptured dpk_eps call of >= N poses before the capture");
+            c->eps.push_back(EpsBuf{st, h->eps_spare.p, h->eps_spare.cap});
+            h->eps_spare = EpsBuf{};
+            mine = &c->eps.back();
+        } else if (mine->cap < N) {
+            return fail(h, DPK_E_STATE, "dpk_eps: the captured calls of one stream share the buffer of the capture's "
+                                        "first call (" + std::to_string(mine->cap) + " poses); this one has " +
+                                        std::to_string(N) + "; warm up with the largest N before capturing");
+        }
+        proj = mine->p;
     } else {
+        cap_sweep(h);
         EpsBuf* buf = nullptr;
         for (auto& b : h->eps_bufs)
             if (b.st == st) buf = &b;
@@ -1053,14 +1224,18 @@ int dpk_eps(dpk_handle* h, const float* x, const float* t, float* eps, int N, vo
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
-    launch_sampler<M_EPS>(h, st, a, cap);
-    HIPCHK(h, hipGetLastError());
+    if ((rc = launch_sampler<M_EPS>(h, st, a, cap))) return rc;
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_eps: event record");
     return DPK_OK;
 }
 
 int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s, int N, uint64_t seed,
                void* stream) {
+    return dpk_sample_noise(h, x, out, xs, x0s, N, seed, nullptr, stream);
+}
+
+int dpk_sample_noise(dpk_handle* h, const float* x, float* out, float* xs, float* x0s, int N, uint64_t seed,
+                     const float* noise, void* stream) {
     if (!h) return DPK_E_INVALID;
     if (N < 0 || (N > 0 && (!x || !out))) return fail(h, DPK_E_INVALID, "dpk_sample: bad args");
     int rc = check_ready(h);
@@ -1076,10 +1251,14 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     bool cap = false;
     rc = capturing(h, st, &cap);
     if (rc) return rc;
-    if (!cap) sched_sweep(h);
-    if (h->gen) return gen_sample(h, sc, x, out, xs, x0s, N, seed, st, cap);
+    if (!cap) {
+        cap_sweep(h);
+        sched_sweep(h);
+    }
+    if (h->gen) return gen_sample(h, sc, x, out, xs, x0s, N, seed, noise, st, cap);
     if (xs) HIPCHK(h, hipMemcpyAsync(xs, x, (size_t)N * PE * 4, hipMemcpyDeviceToDevice, st));
     SampleArgs a{};
+    a.noise = noise;
     a.arena = h->arena;
     a.coef = sc->coef;
     a.tproj = sc->tps;
@@ -1110,8 +1289,7 @@ int dpk_sample(dpk_handle* h, const float* x, float* out, float* xs, float* x0s,
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
-    launch_sampler<M_SAMPLE>(h, st, a, cap);
-    HIPCHK(h, hipGetLastError());
+    if ((rc = launch_sampler<M_SAMPLE>(h, st, a, cap))) return rc;
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_sample: event record");
     return sched_note_use(h, sc, st, cap);
 }
@@ -1147,8 +1325,7 @@ int dpk_pose(dpk_handle* h, const float* x2d, float* xyz, float* uvxyz, int N, i
     const bool prof = h->profiling && !cap;
     std::pair<hipEvent_t, hipEvent_t> ev;
     if (prof && prof_begin(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
-    launch_sampler<M_POSE>(h, st, a, cap);
-    HIPCHK(h, hipGetLastError());
+    if ((rc = launch_sampler<M_POSE>(h, st, a, cap))) return rc;
     if (prof && prof_end(h, st, ev)) return fail(h, DPK_E_HIP, "dpk_pose: event record");
     return DPK_OK;
 }
@@ -1193,6 +1370,11 @@ int dpk_profile_read(dpk_handle* h, float* ms, int cap, int* count) {
 
 int dpk_ddim_update(dpk_handle* h, const float* xt, const float* et, float* xn, float* x0, int64_t n, int step,
                     uint64_t seed, void* stream) {
+    return dpk_ddim_update_noise(h, xt, et, xn, x0, n, step, seed, nullptr, stream);
+}
+
+int dpk_ddim_update_noise(dpk_handle* h, const float* xt, const float* et, float* xn, float* x0, int64_t n,
+                          int step, uint64_t seed, const float* noise, void* stream) {
     if (!h) return DPK_E_INVALID;
     if (n < 0 || (n > 0 && (!xt || !et || !xn))) return fail(h, DPK_E_INVALID, "dpk_ddim_update: bad args");
     Sched* sc = h->sched;
@@ -1204,11 +1386,39 @@ int dpk_ddim_update(dpk_handle* h, const float* xt, const float* et, float* xn, 
     bool cap = false;
     int rc = capturing(h, st, &cap);
     if (rc) return rc;
+    if (!cap) cap_sweep(h);
     const long long nb = (n + 255) / 256;
     hipLaunchKernelGGL(ddim_kernel, dim3((unsigned)nb), dim3(256), 0, st, xt, et, xn, x0, (long long)n,
-                       sc->coef + step * 6, step, sc->eta, (unsigned long long)seed);
+                       sc->coef + step * 6, step, sc->eta, (unsigned long long)seed, noise);
     HIPCHK(h, hipGetLastError());
     return sched_note_use(h, sc, st, cap);
+}
+
+int dpk_debug_split(dpk_handle* h, int mode, int* fallbacks) {
+    if (!h) return DPK_E_INVALID;
+    if (mode < 0 || mode > 2) return fail(h, DPK_E_INVALID, "dpk_debug_split: mode must be 0, 1 or 2");
+    h->split_dbg = mode;
+    if (fallbacks) {
+        HIPCHK(h, hipSetDevice(h->device));
+        HIPCHK(h, hipDeviceSynchronize());
+        int* ctr = reinterpret_cast<int*>(h->flags + (size_t)FLAG_SLOTS * h->n_cu);
+        HIPCHK(h, hipMemcpy(fallbacks, ctr, 4, hipMemcpyDeviceToHost));
+        HIPCHK(h, hipMemset(ctr, 0, 4));
+    }
+    return DPK_OK;
+}
+
+int dpk_debug_resources(dpk_handle* h, int* out, int n) {
+    if (!h || (n > 0 && !out)) return DPK_E_INVALID;
+    int released = 0, tracked = 0, retired = (int)h->retired.size();
+    for (CapRes* c : h->caps) {
+        tracked += c->tracked ? 1 : 0;
+        released += (c->tracked && c->released.load()) ? 1 : 0;
+    }
+    const int v[6] = {(int)h->caps.size(), tracked, released, (int)h->slot_free.size(), retired,
+                      h->eps_spare.cap};
+    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    return DPK_OK;
 }
 
 #if DPK_TRACE

@@ -16,8 +16,11 @@ DPK_OK = 0
 ERRORS = {-1: "DPK_E_INVALID", -2: "DPK_E_UNSUPPORTED", -3: "DPK_E_HIP", -4: "DPK_E_STATE", -5: "DPK_E_WEIGHTS"}
 
 # every symbol include/diffpose_kernels.h declares
-EXPORTS = ("dpk_version", "dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks", "dpk_set_schedule",
-           "dpk_eps", "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_set_tail_plan", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry", "dpk_last_error", "dpk_destroy")
+EXPORTS = ("dpk_version", "dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks",
+           "dpk_set_schedule", "dpk_eps", "dpk_sample", "dpk_sample_noise", "dpk_ddim_update", "dpk_ddim_update_noise",
+           "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode",
+           "dpk_set_tail_plan", "dpk_debug_split", "dpk_debug_resources", "dpk_profile", "dpk_profile_read",
+           "dpk_kernel_geometry", "dpk_last_error", "dpk_destroy")
 
 
 class DpkConfig(ctypes.Structure):
@@ -46,6 +49,18 @@ def lib() -> ctypes.CDLL:
     import torch  # noqa: F401  (binds libamdhip64.so.7 before our library resolves it)
 
     L = ctypes.CDLL(LIB_PATH)
+    if "DPK_LIB" in os.environ:
+        # an A/B build of another version (tools/ab_bench.sh): bind what it exports
+        class _Partial:
+            def __init__(self, lib):
+                self._lib = lib
+
+            def __getattr__(self, name):
+                try:
+                    return getattr(self._lib, name)
+                except AttributeError:
+                    return lambda *a: -2          # DPK_E_UNSUPPORTED: not in that build
+        L = _Partial(L)
     vp, i32, i64, u64, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float)
     L.dpk_version.restype = i32
     L.dpk_create.argtypes = [ctypes.POINTER(DpkConfig), ctypes.POINTER(vp)]
@@ -56,7 +71,11 @@ def lib() -> ctypes.CDLL:
     L.dpk_set_schedule.argtypes = [vp, fp, i32, ctypes.POINTER(i32), i32, ctypes.c_float]
     L.dpk_eps.argtypes = [vp, vp, vp, vp, i32, vp]
     L.dpk_sample.argtypes = [vp, vp, vp, vp, vp, i32, u64, vp]
+    L.dpk_sample_noise.argtypes = [vp, vp, vp, vp, vp, i32, u64, vp, vp]
     L.dpk_ddim_update.argtypes = [vp, vp, vp, vp, vp, i64, i32, u64, vp]
+    L.dpk_ddim_update_noise.argtypes = [vp, vp, vp, vp, vp, i64, i32, u64, vp, vp]
+    L.dpk_debug_split.argtypes = [vp, i32, ctypes.POINTER(i32)]
+    L.dpk_debug_resources.argtypes = [vp, ctypes.POINTER(i32), i32]
     L.dpk_pose.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp]
     L.dpk_pose_metrics.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp]
     L.dpk_gmm_sample.argtypes = [vp, vp, i32, i32, vp, i32, vp, u64, ctypes.c_double, vp, vp, vp, vp]
@@ -70,8 +89,9 @@ def lib() -> ctypes.CDLL:
     L.dpk_last_error.restype = ctypes.c_char_p
     L.dpk_destroy.argtypes = [vp]
     L.dpk_destroy.restype = None
-    for name in ("dpk_create", "dpk_set_graph", "dpk_load_weights", "dpk_set_mask", "dpk_set_pose_masks", "dpk_set_schedule", "dpk_eps",
-                 "dpk_sample", "dpk_ddim_update", "dpk_pose", "dpk_pose_metrics", "dpk_gmm_sample", "dpk_gmm_sample_f64", "dpk_set_gemm_mode", "dpk_profile", "dpk_profile_read", "dpk_kernel_geometry"):
+    for name in EXPORTS:
+        if name in ("dpk_last_error", "dpk_destroy"):
+            continue
         getattr(L, name).restype = i32
     _LIB = L
     return L

@@ -214,6 +214,21 @@ class _HipModel:
             raise ValueError(f"tail plan must be one of {sorted(self.TAIL_PLANS)}, got {plan!r}")
         _lib.check(self._h, "dpk_set_tail_plan", _lib.lib().dpk_set_tail_plan(self._h, self.TAIL_PLANS[plan]))
 
+    def debug_split(self, mode: int = 0, read: bool = False):
+        """Test hook (dpk_debug_split): set the step-split handoff mode; with ``read``, wait for the
+        device and return the number of second halves that recomputed their first half's steps."""
+        n = ctypes.c_int(0)
+        _lib.check(self._h, "dpk_debug_split",
+                   _lib.lib().dpk_debug_split(self._h, int(mode), ctypes.byref(n) if read else None))
+        return n.value if read else None
+
+    def debug_resources(self) -> dict:
+        """Test hook (dpk_debug_resources): capture-owned resources and free flag slots."""
+        buf = (ctypes.c_int * 6)()
+        _lib.check(self._h, "dpk_debug_resources", _lib.lib().dpk_debug_resources(self._h, buf, 6))
+        keys = ("captures", "tracked", "released", "free_slots", "retired_schedules", "eps_spare_poses")
+        return dict(zip(keys, list(buf)))
+
     def profile(self, enable: bool = True) -> None:
         """Bracket each model-kernel launch with HIP events (see dpk_profile)."""
         _lib.check(self._h, "dpk_profile", _lib.lib().dpk_profile(self._h, 1 if enable else 0))
@@ -282,11 +297,20 @@ class HipGCNdiff(_HipModel):
     __call__ = forward
 
     def sample(self, x, seq, betas, eta: float = 0.0, mask=None, seed: int = 0, trajectory: bool = False,
-               out=None):
+               out=None, noise=None):
         """Run the whole DDIM loop on device.  Returns the final x, or (xs, x0s) stacks
-        ([K+1,N,17,5], [K,N,17,5]) when ``trajectory`` is set."""
+        ([K+1,N,17,5], [K,N,17,5]) when ``trajectory`` is set.  ``noise``: None (counter-based
+        draws from ``seed`` when eta > 0) or a [K,N,17,5] float32 device tensor whose slice k is the
+        z of the k-th executed step (the reference's per-step ``torch.randn_like(x)``,
+        common/utils_diff.py:65; see ``utils_diff.draw_noise``)."""
         x = self._check_x(x)
         self.set_schedule(seq, betas, eta)
+        if noise is not None:
+            shape = (self.K,) + tuple(x.shape)
+            if not (torch.is_tensor(noise) and noise.is_cuda and noise.dtype == torch.float32
+                    and tuple(noise.shape) == shape and noise.device == x.device):
+                raise ValueError(f"noise must be a float32 tensor of shape {shape} on {x.device}")
+            noise = noise.contiguous()
         self._sync_mask(mask)
         n = x.shape[0]
         self._check_mask_batch(n)
@@ -298,24 +322,36 @@ class HipGCNdiff(_HipModel):
             x0s = torch.empty((self.K,) + tuple(x.shape), dtype=x.dtype, device=x.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = _lib.lib()
-        rc = L.dpk_sample(self._h, x.data_ptr(), out.data_ptr(), xs.data_ptr() if xs is not None else None,
-                          x0s.data_ptr() if x0s is not None else None, n, ctypes.c_uint64(seed & (2**64 - 1)),
-                          stream)
+        xs_p = xs.data_ptr() if xs is not None else None
+        x0s_p = x0s.data_ptr() if x0s is not None else None
+        seed_c = ctypes.c_uint64(seed & (2**64 - 1))
+        if noise is None:
+            rc = L.dpk_sample(self._h, x.data_ptr(), out.data_ptr(), xs_p, x0s_p, n, seed_c, stream)
+        else:
+            rc = L.dpk_sample_noise(self._h, x.data_ptr(), out.data_ptr(), xs_p, x0s_p, n, seed_c,
+                                    noise.data_ptr(), stream)
         _lib.check(self._h, "dpk_sample", rc)
         if trajectory:
             return xs, x0s
         return out
 
-    def ddim_update(self, xt, et, step: int, seed: int = 0, want_x0: bool = True):
-        """x_{t-1} (and x0) from an external eps for schedule step ``step``."""
+    def ddim_update(self, xt, et, step: int, seed: int = 0, want_x0: bool = True, noise=None):
+        """x_{t-1} (and x0) from an external eps for schedule step ``step``; ``noise``: this step's
+        draw z (shaped like xt, on its device) or None (counter-based from ``seed``)."""
         xt, et = xt.contiguous(), et.contiguous()
+        if noise is not None:
+            if not (torch.is_tensor(noise) and noise.dtype == torch.float32 and noise.shape == xt.shape
+                    and noise.device == xt.device):
+                raise ValueError(f"noise must be a float32 tensor shaped like xt {tuple(xt.shape)} on {xt.device}")
+            noise = noise.contiguous()
         xn = torch.empty_like(xt)
         x0 = torch.empty_like(xt) if want_x0 else None
         stream = torch.cuda.current_stream(xt.device).cuda_stream
         L = _lib.lib()
-        rc = L.dpk_ddim_update(self._h, xt.data_ptr(), et.data_ptr(), xn.data_ptr(),
-                               x0.data_ptr() if x0 is not None else None, xt.numel(), step,
-                               ctypes.c_uint64(seed & (2**64 - 1)), stream)
+        rc = L.dpk_ddim_update_noise(self._h, xt.data_ptr(), et.data_ptr(), xn.data_ptr(),
+                                     x0.data_ptr() if x0 is not None else None, xt.numel(), step,
+                                     ctypes.c_uint64(seed & (2**64 - 1)),
+                                     noise.data_ptr() if noise is not None else None, stream)
         _lib.check(self._h, "dpk_ddim_update", rc)
         return xn, x0
 

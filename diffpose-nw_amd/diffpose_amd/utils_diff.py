@@ -9,6 +9,19 @@ the reference signature and return shape (reference ``common/utils_diff.py:46-68
   (``dpk_sample``) writing the trajectory into two preallocated stacks.
 * any other callable ``model(xt, mask, t, cemd)`` → the loop runs on the host, each
   step's DDIM update in the HIP ``dpk_ddim_update`` kernel.
+
+The noise of ``c1 * randn`` (eta > 0).  The reference draws ``torch.randn_like(x)`` once per step,
+in execution order (``common/utils_diff.py:65``); ``noise=`` selects what z is:
+
+* ``"torch"`` (the default when eta > 0): the same K draws, ``torch.randn_like(x)`` on x's
+  device from torch's default generator, so the trajectory is the reference's under the same seed;
+* ``"torch-cpu"``: the K draws from the CPU generator (the reference run on a CPU), uploaded;
+* ``"philox"``: counter-based draws inside the kernel, keyed by (``seed``, step, element) — no
+  [K,N,17,5] buffer, not the reference's numbers;
+* a [K,N,17,5] tensor: slice k is step k's z.
+
+At eta = 0 the noise term is 0·z and nothing is drawn unless ``noise`` asks for it (the reference
+still advances torch's RNG by K draws there; ``noise="torch"`` reproduces that too).
 """
 from __future__ import annotations
 
@@ -28,13 +41,39 @@ def compute_alpha(beta, t):
     return out.to(beta.device) if torch.is_tensor(beta) else out
 
 
+NOISE_SOURCES = ("torch", "torch-cpu", "philox")
+
+
+def draw_noise(x, K: int, source="torch", generator=None):
+    """The K per-step draws z of the reference's ``torch.randn_like(x)`` (common/utils_diff.py:65) as
+    one [K, *x.shape] float32 tensor on x's device, in execution order; None for "philox" / None
+    (the kernel's counter-based draws).  A tensor ``source`` is checked and returned."""
+    if source is None or (isinstance(source, str) and source == "philox"):
+        return None
+    shape = (int(K),) + tuple(x.shape)
+    if torch.is_tensor(source):
+        if tuple(source.shape) != shape:
+            raise ValueError(f"noise must have shape {shape}, got {tuple(source.shape)}")
+        return source.to(device=x.device, dtype=torch.float32).contiguous()
+    if source == "torch":
+        if generator is not None:
+            return torch.stack([torch.randn(x.shape, generator=generator, device=x.device) for _ in range(K)])
+        return torch.stack([torch.randn_like(x, dtype=torch.float32) for _ in range(K)])
+    if source == "torch-cpu":
+        draws = [torch.randn(tuple(x.shape), generator=generator) if generator is not None
+                 else torch.randn(tuple(x.shape)) for _ in range(K)]
+        return torch.stack(draws).to(x.device)
+    raise ValueError(f"noise must be one of {NOISE_SOURCES}, None or a tensor, got {source!r}")
+
+
 def generalized_steps(x, src_mask, seq, model, b, **kwargs):
     eta = float(kwargs.get("eta", 0))
     seed = int(kwargs.get("seed", 0))
     seq = [int(s) for s in seq]
     with torch.no_grad():
+        noise = draw_noise(x, len(seq), kwargs.get("noise", "torch" if eta != 0 else None), kwargs.get("generator"))
         if isinstance(model, HipGCNdiff):
-            xs_t, x0s_t = model.sample(x, seq, b, eta=eta, mask=src_mask, seed=seed, trajectory=True)
+            xs_t, x0s_t = model.sample(x, seq, b, eta=eta, mask=src_mask, seed=seed, trajectory=True, noise=noise)
             return [x] + [xs_t[k] for k in range(1, xs_t.shape[0])], [x0s_t[k] for k in range(x0s_t.shape[0])]
         # generic callable: host loop, HIP DDIM update
         upd = kwargs.get("updater")
@@ -47,7 +86,7 @@ def generalized_steps(x, src_mask, seq, model, b, **kwargs):
         for step, (i, _j) in enumerate(step_pairs(seq)):
             t = torch.full((n,), float(i), device=x.device)
             et = model(xs[-1], src_mask, t, 0)
-            xn, x0 = upd.ddim_update(xs[-1], et, step, seed=seed)
+            xn, x0 = upd.ddim_update(xs[-1], et, step, seed=seed, noise=None if noise is None else noise[step])
             x0s.append(x0)
             xs.append(xn)
         return xs, x0s

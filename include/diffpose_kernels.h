@@ -26,15 +26,18 @@
  *   - Graph capture (hipStreamBeginCapture / torch.cuda.graph): dpk_sample, dpk_eps, dpk_pose
  *     and dpk_ddim_update may be captured.  A captured launch reads the schedule current at
  *     capture time for the graph's whole life (a later dpk_set_schedule builds a new one and
- *     leaves the captured one in place; it is freed by dpk_destroy); weights reloaded later
- *     are seen by replays.  It also keeps the key mask it was captured with: the
- *     dpk_set_mask bits by value, and the dpk_set_pose_masks array by address (that array
- *     must stay allocated and unchanged while the graph may replay).  Nothing is allocated
- *     inside a captured call: each captured dpk_eps takes a projection buffer of its own
- *     (kept until dpk_destroy, so graphs captured on one stream can replay concurrently and
- *     later uncaptured calls of any size cannot disturb them); that buffer comes from a spare
- *     which every uncaptured dpk_eps of at least N poses refills, so one such call must come
- *     before each capture (else DPK_E_STATE).
+ *     leaves the captured one in place); weights reloaded later are seen by replays.  It also
+ *     keeps the key mask it was captured with: the dpk_set_mask bits by value, and the
+ *     dpk_set_pose_masks array by address (that array must stay allocated and unchanged while
+ *     the graph may replay).  Nothing is allocated inside a captured call.  What the launches of
+ *     one capture read by address (their schedules, one dpk_eps projection buffer and one
+ *     step-split flag slot per capturing stream, shared by that stream's captured calls) belongs
+ *     to the capture: a user object retained by the captured graph releases it when the graph and
+ *     its executable instances are destroyed, and the handle's next uncaptured call recycles it
+ *     (after one device-wide wait).  The first captured dpk_eps of a capture takes the handle's
+ *     spare projection buffer, which every uncaptured dpk_eps of at least N poses sizes: make one
+ *     with the capture's largest N before it (else DPK_E_STATE).  Replays of one executable graph
+ *     must not overlap each other (HIP orders launches of the same graph exec).
  */
 #ifndef DIFFPOSE_KERNELS_H
 #define DIFFPOSE_KERNELS_H
@@ -135,11 +138,24 @@ int dpk_eps(dpk_handle* h, const float* x_dev, const float* t_dev, float* eps_de
 int dpk_sample(dpk_handle* h, const float* x_dev, float* out_dev, float* xs_dev, float* x0s_dev,
                int N, uint64_t seed, void* stream);
 
+/* dpk_sample with the caller's noise for eta > 0: noise_dev [K,N,17,5] fp32 device, slice k the
+ * draw z of the k-th executed step (t = seq[K-1-k]) in x' = sqrt(an)*x0 + c1*z + c2*et — what the
+ * reference draws as torch.randn_like(x) once per step (common/utils_diff.py:65), so a caller that
+ * draws the same K tensors reproduces the reference's eta > 0 trajectory.  NULL = counter-based
+ * noise from `seed` (dpk_sample).  Read asynchronously on `stream`. */
+int dpk_sample_noise(dpk_handle* h, const float* x_dev, float* out_dev, float* xs_dev, float* x0s_dev,
+                     int N, uint64_t seed, const float* noise_dev, void* stream);
+
 /* One DDIM update for an externally computed eps (generic model callables):
  * the per-element body of common/utils_diff.py:59-65 for schedule step `step`
  * (0 = first executed step, t = seq[K-1]).  x0_out may be NULL. */
 int dpk_ddim_update(dpk_handle* h, const float* xt_dev, const float* eps_dev, float* xnext_dev,
                     float* x0_dev, int64_t n_elems, int step, uint64_t seed, void* stream);
+
+/* dpk_ddim_update with this step's draw z (noise_dev [n_elems] fp32 device; NULL = counter-based). */
+int dpk_ddim_update_noise(dpk_handle* h, const float* xt_dev, const float* eps_dev, float* xnext_dev,
+                          float* x0_dev, int64_t n_elems, int step, uint64_t seed, const float* noise_dev,
+                          void* stream);
 
 /* GCNpose front-end (models/gcnpose.py:55-113) for a handle created with coords_in 2,
  * coords_out 3 (create_pose_model, runners/diffpose_frame.py:134-154), fused with the
@@ -220,12 +236,13 @@ int dpk_set_gemm_mode(dpk_handle* h, int mode);
  *           first half's x_t handed over through `out` and a device flag), so the last round
  *           costs about half a round; otherwise plan 1.
  * Plans 0 and 2 give bitwise the same outputs (the same tiles, the same per-step arithmetic);
- * plan 1 agrees within fp32 rounding (other rows on the 4-row tail path).  Plan 2 needs a flag
- * slot: one per caller stream for uncaptured calls and one per captured call, 64 per handle,
- * never released before dpk_destroy (a caller cycling through many short-lived streams uses
- * them up); a call that finds none left runs plan 1.  A second half waits for its first half
- * at most ~8 s (a first half that never arrives: that tile's output is NaN, not a hang).  dpk_eps and dpk_pose (one step) use plan 1 for
- * plan 2.  The environment variable DPK_TAIL_SPLIT sets the initial plan of a new handle. */
+ * plan 1 agrees within fp32 rounding (other rows on the 4-row tail path).  The plan-2 handoff
+ * assumes no dispatch order: a second half whose first half has not started after a few ms runs
+ * the whole tile itself (correct output, only slower; dpk_debug_split counts these), and a first
+ * half that then starts leaves without writing.  Plan 2 needs one of 64 flag slots per handle: an
+ * uncaptured call holds one until its launch has completed, a capture one per capturing stream
+ * for the graph's life; a call that finds none free runs plan 1.  dpk_eps and dpk_pose (one step)
+ * use plan 1 for plan 2.  The environment variable DPK_TAIL_SPLIT sets a new handle's plan. */
 int dpk_set_tail_plan(dpk_handle* h, int plan);
 
 /* Launch timing of the sampler kernel itself: with enable != 0, every dpk_sample /
@@ -234,6 +251,17 @@ int dpk_set_tail_plan(dpk_handle* h, int plan);
  * `cap` elapsed times in ms (oldest first), then clears them. */
 int dpk_profile(dpk_handle* h, int enable);
 int dpk_profile_read(dpk_handle* h, float* ms_out, int cap, int* count);
+
+/* Test hooks (not part of the reference interface).
+ * dpk_debug_split: mode 0 normal; 1: step-split first halves start ~100 ms late and second halves
+ * do not wait for an unstarted first half, so every split tile takes the recompute path; 2: second
+ * halves do not wait for an unstarted first half.  With `fallbacks` non-NULL, waits for the device
+ * and returns (then clears) the number of second halves that ran their tile's first-half steps.
+ * dpk_debug_resources: out[0..5] = captures holding resources, captures whose graph holds our
+ * user object, captures released (graph gone, not yet recycled), free flag slots, retired
+ * schedules, spare dpk_eps capacity (poses). */
+int dpk_debug_split(dpk_handle* h, int mode, int* fallbacks);
+int dpk_debug_resources(dpk_handle* h, int* out, int n);
 
 /* Poses per workgroup of the sampler kernel and its static LDS bytes (for docs/bench). */
 int dpk_kernel_geometry(int* poses_per_workgroup, int* threads_per_workgroup, int* lds_bytes);

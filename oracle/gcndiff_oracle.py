@@ -205,14 +205,16 @@ def alpha_at(b: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
 
 
 def generalized_steps(x: torch.Tensor, mask, seq, eps_fn, b: torch.Tensor, eta: float = 0.0,
-                      generator: torch.Generator | None = None):
-    """DDIM reverse loop; returns (xs[K+1], x0_preds[K]) (common/utils_diff.py:46-68)."""
+                      generator: torch.Generator | None = None, noise: torch.Tensor | None = None):
+    """DDIM reverse loop; returns (xs[K+1], x0_preds[K]) (common/utils_diff.py:46-68).  The z of
+    step k is ``torch.randn_like(x)`` as in the reference (global RNG, or ``generator``), or
+    ``noise[k]`` when a [K, *x.shape] tensor is given."""
     with torch.no_grad():
         n = x.size(0)
         seq = list(seq)
         seq_next = [-1] + seq[:-1]
         xs, x0s = [x], []
-        for i, j in zip(reversed(seq), reversed(seq_next)):
+        for k, (i, j) in enumerate(zip(reversed(seq), reversed(seq_next))):
             t = torch.ones(n) * i
             tn = torch.ones(n) * j
             at, an = alpha_at(b, t.long()), alpha_at(b, tn.long())
@@ -222,8 +224,11 @@ def generalized_steps(x: torch.Tensor, mask, seq, eps_fn, b: torch.Tensor, eta: 
             x0s.append(x0)
             c1 = eta * ((1 - at / an) * (1 - an) / (1 - at)).sqrt()
             c2 = ((1 - an) - c1 ** 2).sqrt()
-            noise = torch.randn(x.shape, generator=generator) if generator is not None else torch.randn_like(x)
-            xs.append(an.sqrt() * x0 + c1 * noise + c2 * et)
+            if noise is not None:
+                z = noise[k].to(x.dtype)
+            else:
+                z = torch.randn(x.shape, generator=generator) if generator is not None else torch.randn_like(x)
+            xs.append(an.sqrt() * x0 + c1 * z + c2 * et)
     return xs, x0s
 
 

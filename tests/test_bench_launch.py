@@ -62,6 +62,18 @@ def test_bench_config4_eight_ranks_cpu_dry():
     assert len(line["per_rank_ms"]) == 8
     assert line["reassembly_ok"] is True
     assert line["allgather_ms"] > 0
+    # the final MPJPE reduction: per-frame errors of all 8 shards gathered (16 B per frame) equal the
+    # MPJPE of the stub output over the whole batch computed in one process
+    import numpy as np
+
+    from diffpose_amd.data import synthetic_batch
+
+    x, tgt = synthetic_batch(8192)
+    o = 2.0 * x.astype(np.float64)[:, :, 2:]
+    ref = float(np.mean(np.linalg.norm(o - o[:, :1] - tgt.astype(np.float64), axis=-1))) * 1000.0
+    m = line["mpjpe"]
+    assert m["frames"] == 8192 and "all_gather" in m["how"]
+    assert abs(m["p1_mm"] - ref) <= 1e-6 * max(1.0, ref)
 
 
 def test_bench_config5_eight_ranks_cpu_dry():

@@ -4,13 +4,14 @@ rank r of the 8-GPU run computes) run one after another on this GPU, are reassem
 dist.shard_rows order, and must equal the unsharded 8,192-frame run bit for bit: every pose's result
 depends only on its own workgroup tile, and each shard starts on a tile boundary.  Frames drawn
 from every shard are checked against the golden-pinned oracle at the fp32 bars of
-test_gpu_parity.py (elementwise 2e-5, MPJPE 1e-4 mm).
+test_gpu_parity.py (elementwise 5e-6, MPJPE 1e-4 mm).
 Reference: runners/diffpose_frame.py:126-127 (one DataParallel replica), :342 (hypothesis-major
 rows), common/utils_diff.py:46-68 (the loop each rank runs)."""
 import numpy as np
 import pytest
 import torch
 
+from conftest import record_delta
 from diffpose_amd import dist as D
 from diffpose_amd.data import shard_frames, synthetic_batch
 from diffpose_amd.gcndiff import HipGCNdiff, adj_mx_from_edges
@@ -67,5 +68,5 @@ def test_config4_eight_shards_equal_unsharded_and_oracle():
     dm = abs(_mpjpe_mm(hip, tgt[sel]) - _mpjpe_mm(ref, tgt[sel]))
     print(f"\nconfig 4: 8 shards of 1024 == unsharded 8192 bitwise; oracle on {sel.size} frames: "
           f"max|d| {d:.3e}, MPJPE d {dm:.3e} mm")
-    assert d <= 2e-5
-    assert dm <= 1e-4
+    assert record_delta(d, 5e-6)
+    assert record_delta(dm, 1e-4)

@@ -75,3 +75,45 @@ def test_gather_frames_over_rccl_world1():
                        timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "GATHER_OK" in r.stdout
+
+
+_HYBER = r"""
+import torch, torch.distributed as dist
+from diffpose_amd import runner as R
+from diffpose_amd.data import synthetic_eval_batches
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+
+def run(eta):
+    cfg = R.default_config(test_times=2, test_timesteps=10, test_num_diffusion_timesteps=50, batch_size=96)
+    d = R.Diffpose(R.default_args(eta=eta), cfg, device=dev)
+    d.create_diffusion_model()
+    d.create_pose_model()
+    torch.manual_seed(3)
+    p = d.test_hyber(batches=list(synthetic_eval_batches(300, 96, seed=9)), is_train=1)
+    acc = {a: (v["p1"].sum, v["p1"].count, v["p2"].sum, v["p2"].count) for a, v in d.action_error_sum.items()}
+    return p, acc, d.epoch_loss
+
+plain = {eta: run(eta) for eta in (0.0, 0.5)}          # one process, no collective
+dist.init_process_group("nccl", device_id=dev)
+for eta in (0.0, 0.5):
+    got = run(eta)                                       # the distributed path: per-frame all-gather over RCCL
+    assert got == plain[eta], (eta, got[0], plain[eta][0])
+assert plain[0.5][0] != plain[0.0][0]
+dist.destroy_process_group()
+print("HYBER_OK", plain[0.0][0], plain[0.5][0])
+"""
+
+
+def test_runner_test_hyber_over_rccl_world1_equals_plain_run():
+    """runner.Diffpose.test_hyber through its distributed code (frame shard, pose + sampler +
+    per-frame metrics, the RCCL all-gather of per-frame (p1, p2), the unchanged accounting) at
+    world size 1 gives exactly the plain single-process result, at eta 0 and at eta 0.5 with the
+    reference's per-step randn_like draws (runners/diffpose_frame.py:330-420)."""
+    env = _env()
+    env.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-c", _HYBER], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "HYBER_OK" in r.stdout
+    print(r.stdout.strip().splitlines()[-1])

@@ -2,15 +2,19 @@
 the golden-pinned CPU oracle.
 
 Tolerances (fp32 everywhere; the HIP path reorders fp32 sums — MFMA k-order, fused
-Chebyshev GEMM, double-accumulated LayerNorm statistics — so it is not bitwise):
-  * single denoiser call: |eps - eps_ref| <= 2e-5 (|eps| ~ 1);
-  * trajectories: |x - x_ref| <= 2e-5 elementwise;
+Chebyshev GEMM, double-accumulated LayerNorm statistics — so it is not bitwise).  Round 4 set
+them from what the kernel achieves (every check reports its delta through
+``conftest.record_delta``; the GPU run's log is kept under profiles/):
+  * single denoiser call: |eps - eps_ref| <= 5e-6 (|eps| ~ 1);
+  * trajectories: |x - x_ref| <= 5e-6 elementwise;
   * north-star bar: |MPJPE_hip - MPJPE_ref| <= 1e-4 mm at B=1024, K=50.
 The reference's own fp32-vs-fp64 gap on these inputs is 1.6e-5 mm / 1.2e-6 per element.
 """
 import numpy as np
 import pytest
 import torch
+
+from conftest import record_delta
 
 from diffpose_amd.schedule import get_beta_schedule, make_seq
 from diffpose_amd.weights import synthetic_state_dict
@@ -20,8 +24,8 @@ from diffpose_amd import utils_diff
 
 pytestmark = pytest.mark.gpu
 
-EPS_TOL = 2e-5
-TRAJ_TOL = 2e-5
+EPS_TOL = 5e-6
+TRAJ_TOL = 5e-6
 MPJPE_TOL_MM = 1e-4
 
 
@@ -64,12 +68,12 @@ def test_eps_vs_golden(model, mask, golden):
     x = torch.from_numpy(g["x"]).cuda()
     t = torch.from_numpy(g["t"]).cuda()
     eps = model(x, mask, t, 0)
-    assert _maxdiff(eps, g["eps"]) <= EPS_TOL
+    assert record_delta(_maxdiff(eps, g["eps"]), EPS_TOL)
     m2 = torch.from_numpy(g["mask2"]).cuda()
     eps2 = model(x, m2, t, 0)
-    assert _maxdiff(eps2, g["eps_masked"]) <= EPS_TOL
+    assert record_delta(_maxdiff(eps2, g["eps_masked"]), EPS_TOL)
     eps3 = model(x, mask, t, 0)                      # mask restored
-    assert _maxdiff(eps3, g["eps"]) <= EPS_TOL
+    assert record_delta(_maxdiff(eps3, g["eps"]), EPS_TOL)
 
 
 def test_trajectory_vs_golden(model, mask, golden):
@@ -77,9 +81,9 @@ def test_trajectory_vs_golden(model, mask, golden):
     x = torch.from_numpy(g["x"]).cuda()
     xs, x0s = utils_diff.generalized_steps(x, mask, [int(s) for s in g["seq"]], model, _betas(51).cuda(), eta=0.0)
     assert xs[0] is x and len(xs) == 11 and len(x0s) == 10
-    assert _maxdiff(torch.stack(xs), g["xs"]) <= TRAJ_TOL
-    assert _maxdiff(torch.stack(x0s), g["x0s"]) <= TRAJ_TOL
-    assert abs(_mpjpe_mm(xs[-1], g["targets"]) - float(g["mpjpe_mm"])) <= MPJPE_TOL_MM
+    assert record_delta(_maxdiff(torch.stack(xs), g["xs"]), TRAJ_TOL)
+    assert record_delta(_maxdiff(torch.stack(x0s), g["x0s"]), TRAJ_TOL)
+    assert record_delta(abs(_mpjpe_mm(xs[-1], g["targets"]) - float(g["mpjpe_mm"])), MPJPE_TOL_MM)
 
 
 @pytest.mark.parametrize("name", ["g4_final_n16_k50.npz", "g4_final_n16_k100_T101.npz", "g4_final_n8_quad.npz"])
@@ -87,8 +91,8 @@ def test_final_vs_golden(model, mask, golden, name):
     g = golden(name)
     x = torch.from_numpy(g["x"]).cuda()
     out = model.sample(x, [int(s) for s in g["seq"]], _betas(int(g["T"])), mask=mask)
-    assert _maxdiff(out, g["out"]) <= TRAJ_TOL
-    assert abs(_mpjpe_mm(out, g["targets"]) - _mpjpe_mm(g["out"], g["targets"])) <= MPJPE_TOL_MM
+    assert record_delta(_maxdiff(out, g["out"]), TRAJ_TOL)
+    assert record_delta(abs(_mpjpe_mm(out, g["targets"]) - _mpjpe_mm(g["out"], g["targets"])), MPJPE_TOL_MM)
 
 
 def test_bench_config_vs_oracle(model, mask):
@@ -104,8 +108,8 @@ def test_bench_config_vs_oracle(model, mask):
     xs, _ = O.generalized_steps(torch.from_numpy(x), torch.ones(1, 1, 17, dtype=torch.bool), seq,
                                 lambda a, m, t: O.gcndiff_forward(P, adj, a, m, t), _betas(51))
     ref = xs[-1]
-    assert _maxdiff(out, ref) <= TRAJ_TOL
-    assert abs(_mpjpe_mm(out, tgt) - _mpjpe_mm(ref, tgt)) <= MPJPE_TOL_MM
+    assert record_delta(_maxdiff(out, ref), TRAJ_TOL)
+    assert record_delta(abs(_mpjpe_mm(out, tgt) - _mpjpe_mm(ref, tgt)), MPJPE_TOL_MM)
 
 
 def test_generic_callable_path(model, mask):
@@ -176,14 +180,14 @@ def test_tail_round_plans(model, mask):
         tail = model.sample(xt[2048:].contiguous(), seq, _betas(51), mask=mask)
         assert torch.equal(out1[:2048], head) and torch.equal(out1[2048:], tail)
         assert torch.equal(out4[:2048], head)
-        assert _maxdiff(out1, out) <= TRAJ_TOL
+        assert record_delta(_maxdiff(out1, out), TRAJ_TOL)
     finally:
         model.set_tail_plan("step_split")
     P, adj = O.params_to_torch(synthetic_state_dict()), O.adjacency()
     sel = torch.tensor([2048, 2049, 2050, 2051, 2558, 2559])
     xs, _ = O.generalized_steps(torch.from_numpy(x)[sel], torch.ones(1, 1, 17, dtype=torch.bool), seq,
                                 lambda a_, m_, t_: O.gcndiff_forward(P, adj, a_, m_, t_), _betas(51))
-    assert _maxdiff(out[sel.cuda()], xs[-1]) <= TRAJ_TOL
+    assert record_delta(_maxdiff(out[sel.cuda()], xs[-1]), TRAJ_TOL)
 
 
 @pytest.mark.parametrize("n,k", [(1101, 25), (1100, 2), (2048 + 4 * 128, 50), (1025, 10), (1536, 10),
@@ -221,8 +225,111 @@ def test_step_split_quad_schedule(model, mask):
         model.set_tail_plan("step_split")
 
 
+def test_eta_reference_noise_vs_golden(model, mask, golden):
+    """eta > 0 pinned to the reference (golden g11: the reference's generalized_steps under
+    torch.manual_seed, common/utils_diff.py:65 drawing randn_like once per step).  The HIP sampler
+    given those K draws (dpk_sample_noise) follows the reference trajectory within the fp32 bars;
+    ``generalized_steps(noise="torch-cpu")`` under the same seed draws the same tensors (bitwise the
+    explicit run); the host-loop path (generic callable + dpk_ddim_update_noise) matches too; and
+    K=50 at eta=1 stays within the MPJPE bar."""
+    g = golden("g11_eta.npz")
+    x = torch.from_numpy(g["x"]).cuda()
+    seq10 = [int(s) for s in g["seq10"]]
+    eta = float(g["eta10"])
+    noise = torch.from_numpy(g["noise10"]).cuda()
+    xs, x0s = model.sample(x, seq10, _betas(51), eta=eta, mask=mask, trajectory=True, noise=noise)
+    assert record_delta(_maxdiff(xs, g["xs10"]), TRAJ_TOL)
+    assert record_delta(_maxdiff(x0s, g["x0s10"]), TRAJ_TOL)
+    assert record_delta(abs(_mpjpe_mm(xs[-1], g["targets"]) - _mpjpe_mm(g["xs10"][-1], g["targets"])), MPJPE_TOL_MM)
+    torch.manual_seed(int(g["seed10"]))
+    xs_t, _ = utils_diff.generalized_steps(x, mask, seq10, model, _betas(51), eta=eta, noise="torch-cpu")
+    assert torch.equal(xs_t[-1], xs[-1])
+    fwd = lambda a_, m_, t_, c_: model(a_, m_, t_, c_)   # noqa: E731  (a plain callable: host loop)
+    xs_h, _ = utils_diff.generalized_steps(x, mask, seq10, fwd, _betas(51), eta=eta, noise=noise)
+    assert record_delta(_maxdiff(torch.stack(xs_h), g["xs10"]), TRAJ_TOL)
+    seq50 = [int(s) for s in g["seq50"]]
+    out50 = model.sample(x, seq50, _betas(51), eta=float(g["eta50"]), mask=mask,
+                         noise=torch.from_numpy(g["noise50"]).cuda())
+    assert record_delta(_maxdiff(out50, g["out50"]), TRAJ_TOL)
+    assert record_delta(abs(_mpjpe_mm(out50, g["targets"]) - _mpjpe_mm(g["out50"], g["targets"])), MPJPE_TOL_MM)
+    with pytest.raises(ValueError):
+        model.sample(x, seq10, _betas(51), eta=eta, mask=mask, noise=noise[:5])
+    model.set_schedule(seq10, _betas(51), eta=0.0)
+
+
+def test_step_split_with_noise_and_fallback(model, mask):
+    """Caller noise through the step split (1,100 poses: 19 split tiles after one full round) is
+    bitwise plan "four"'s.  The handoff's fallback (dpk_debug_split 1: first halves start ~100 ms
+    late and second halves do not wait for an unstarted one) makes every second half run its whole
+    tile from x_in: same bits, and the library counts 19 fallbacks; mode 2 (no idle wait, first
+    halves on time) may take either path per tile, same bits.  A first half that starts after its
+    second half gave up writes nothing (the outputs would differ otherwise)."""
+    x, _ = synthetic_batch(1100, seed=37)
+    xt = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, 10)
+    noise = torch.randn((10,) + tuple(xt.shape), generator=torch.Generator().manual_seed(4)).cuda()
+    try:
+        model.set_tail_plan("four")
+        ref = model.sample(xt, seq, _betas(51), eta=0.7, mask=mask, noise=noise)
+        ref0 = model.sample(xt, seq, _betas(51), mask=mask)
+        model.set_tail_plan("step_split")
+        assert model.debug_split(0, read=True) >= 0          # clear the counter
+        assert torch.equal(model.sample(xt, seq, _betas(51), eta=0.7, mask=mask, noise=noise), ref)
+        assert model.debug_split(0, read=True) == 0
+        model.debug_split(1)
+        assert torch.equal(model.sample(xt, seq, _betas(51), eta=0.7, mask=mask, noise=noise), ref)
+        assert torch.equal(model.sample(xt, seq, _betas(51), mask=mask), ref0)
+        n_fb = model.debug_split(2, read=True)
+        print(f"\nstep split fallback (mode 1): {n_fb} of 2 x 19 second halves recomputed")
+        assert n_fb == 2 * 19
+        assert torch.equal(model.sample(xt, seq, _betas(51), mask=mask), ref0)
+        assert 0 <= model.debug_split(0, read=True) <= 19
+        assert torch.equal(model.sample(xt, seq, _betas(51), mask=mask), ref0)   # back to normal: flags clean
+        assert model.debug_split(0, read=True) == 0
+    finally:
+        model.debug_split(0)
+        model.set_tail_plan("step_split")
+        model.set_schedule(seq, _betas(51), eta=0.0)
+
+
+def test_step_split_slots_recycled_across_streams(model, mask):
+    """Flag slots are held per launch, not per stream: 80 short-lived HIP streams (more than the 64
+    slots; destroyed after use, so addresses recur) each run a step-split launch; every one runs plan 2 (bitwise plan "four") and all 64
+    slots are free again once the launches have completed."""
+    x, _ = synthetic_batch(1100, seed=41)
+    xt = torch.from_numpy(x).cuda()
+    seq = make_seq("uniform", 50, 2)
+    try:
+        model.set_tail_plan("four")
+        ref = model.sample(xt, seq, _betas(51), mask=mask)
+        model.set_tail_plan("step_split")
+        import ctypes
+
+        hip = ctypes.CDLL("libamdhip64.so")
+        torch.cuda.synchronize()
+        outs = []
+        for _ in range(80):                    # raw HIP streams (torch's own come from a pool of 32)
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+            es = torch.cuda.ExternalStream(h.value)
+            o = torch.empty_like(xt)                # allocated on torch's stream, written on es
+            torch.cuda.synchronize()
+            with torch.cuda.stream(es):
+                model.sample(xt, seq, _betas(51), mask=mask, out=o)
+            es.synchronize()
+            outs.append(o)
+            assert hip.hipStreamDestroy(h) == 0     # a later stream may reuse the address
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, ref) for o in outs)
+        model.sample(xt, seq, _betas(51), mask=mask)      # sweeps the completed launches
+        torch.cuda.synchronize()
+        assert model.debug_resources()["free_slots"] >= 63
+    finally:
+        model.set_tail_plan("step_split")
+
+
 def test_eta_noise_statistics(model, mask):
-    """eta > 0 draws N(0,1) noise in-kernel (counter-based; not torch.randn_like): check
+    """eta > 0 with the in-kernel counter-based draws (noise="philox"; not torch.randn_like): check
     determinism per seed and the moments of the recovered noise (parity is statistical)."""
     x, _ = synthetic_batch(4096, seed=1)
     x = torch.from_numpy(x).cuda()
@@ -269,13 +376,13 @@ def test_non_h36m_graph_dense_path(mask):
     eps = m(torch.from_numpy(x).cuda(), mask, t.cuda(), 0)
     ref = O.gcndiff_forward(O.params_to_torch(sd), O.adjacency(17, edges), torch.from_numpy(x),
                             torch.ones(1, 1, 17, dtype=torch.bool), t)
-    assert _maxdiff(eps, ref) <= EPS_TOL
+    assert record_delta(_maxdiff(eps, ref), EPS_TOL)
     seq = make_seq("uniform", 50, 10)
     out = m.sample(torch.from_numpy(x).cuda(), seq, _betas(51), mask=mask)
     xs, _ = O.generalized_steps(torch.from_numpy(x), torch.ones(1, 1, 17, dtype=torch.bool), seq,
                                 lambda a_, m_, t_: O.gcndiff_forward(O.params_to_torch(sd), O.adjacency(17, edges),
                                                                      a_, m_, t_), _betas(51))
-    assert _maxdiff(out, xs[-1]) <= TRAJ_TOL
+    assert record_delta(_maxdiff(out, xs[-1]), TRAJ_TOL)
 
 
 def test_temb_cache_follows_schedule_and_weights(mask):

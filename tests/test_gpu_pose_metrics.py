@@ -5,13 +5,15 @@
 * dpk_pose_metrics vs the reference's per-frame P-MPJPE golden (g7) and the oracle;
 * runner.Diffpose.test_hyber end to end vs the oracle pipeline.
 
-Tolerances: GCNpose output |xyz - ref| <= 2e-5 (one backbone pass, like eps); per-frame
+Tolerances: GCNpose output |xyz - ref| <= 5e-6 (one backbone pass, like eps); per-frame
 P-MPJPE within 1e-7 m of the reference's float32-numpy values (its own rounding is ~3e-8 m);
 MPJPE within 1e-9 relative of the fp64 oracle; end-to-end p1/p2 within 1e-4 mm.
 """
 import numpy as np
 import pytest
 import torch
+
+from conftest import record_delta
 
 from diffpose_amd import metrics
 from diffpose_amd.gcndiff import adj_mx_from_edges
@@ -20,7 +22,7 @@ from diffpose_amd.weights import synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 
-POSE_TOL = 2e-5
+POSE_TOL = 5e-6
 
 
 @pytest.fixture(scope="module")
@@ -41,13 +43,13 @@ def test_gcnpose_vs_golden(pose_model, golden):
     g = golden("g6_gcnpose.npz")
     x2d = torch.from_numpy(g["x2d"]).cuda()
     xyz = pose_model(x2d, _mask())
-    assert float((xyz.cpu() - torch.from_numpy(g["xyz"])).abs().max()) <= POSE_TOL
+    assert record_delta(float((xyz.cpu() - torch.from_numpy(g["xyz"])).abs().max()), POSE_TOL)
     xyz_m = pose_model(x2d, _mask(g["mask2"]))
-    assert float((xyz_m.cpu() - torch.from_numpy(g["xyz_masked"])).abs().max()) <= POSE_TOL
+    assert record_delta(float((xyz_m.cpu() - torch.from_numpy(g["xyz_masked"])).abs().max()), POSE_TOL)
     uvxyz, raw = pose_model.uvxyz(x2d, _mask(), test_times=3, root_mode="quirk", return_xyz=True)
     ref = torch.from_numpy(g["uvxyz_h3"])
     assert torch.equal(uvxyz.cpu()[..., :2], ref[..., :2])                    # uv copied exactly
-    assert float((uvxyz.cpu() - ref).abs().max()) <= POSE_TOL
+    assert record_delta(float((uvxyz.cpu() - ref).abs().max()), POSE_TOL)
     assert torch.equal(uvxyz[:12], uvxyz[12:24]) and torch.equal(uvxyz[:12], uvxyz[24:])
     assert torch.all(uvxyz[:, 0, 2:] == 0)
     assert torch.equal(raw, xyz)
@@ -64,7 +66,7 @@ def test_gcnpose_root_modes(pose_model, mode):
     xyz_ref = O.gcnpose_forward(P, O.adjacency(), x2d, torch.ones(1, 1, 17, dtype=torch.bool))
     ref = O.build_uvxyz(x2d, xyz_ref, 2, mode)
     out = pose_model.uvxyz(x2d.cuda(), _mask(), test_times=2, root_mode=mode)
-    assert float((out.cpu() - ref).abs().max()) <= POSE_TOL
+    assert record_delta(float((out.cpu() - ref).abs().max()), POSE_TOL)
     if mode == "relative":
         assert torch.all(out[:, 0, 2:] == 0)
 

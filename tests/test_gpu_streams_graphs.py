@@ -123,8 +123,8 @@ def test_step_split_on_three_streams_without_sync(dev):
 
 
 def test_flag_slots_exhausted_fall_back_to_two_pose_tiles(dev):
-    """A handle has 64 flag slots; captured step-split launches keep theirs for good.  Once they
-    are gone a capture runs the 2-pose tail plan instead (bitwise that plan's eager result), and
+    """A handle has 64 flag slots; a capture keeps its slot while its graph lives (these graphs all
+    stay alive).  Once they are gone a capture runs the 2-pose tail plan instead (bitwise that plan's eager result), and
     the graphs captured earlier still replay the step-split result."""
     m = _model(dev)
     x = torch.from_numpy(synthetic_batch(1100, seed=16)[0]).to(dev)
@@ -331,4 +331,99 @@ def test_captured_eps_without_spare_is_refused(dev):
     torch.cuda.synchronize()
     ref = _model(dev)(x, mask, t, 0)
     assert torch.equal(m(x, mask, t, 0), ref)
+    m.close()
+
+
+def test_capture_of_an_eps_loop_replays_bitwise(dev):
+    """advisor r03 (medium): one capture holding several dpk_eps calls — generalized_steps over a
+    plain callable (host loop: model(x, mask, t) then the DDIM update, K=4 steps, so 4 captured
+    dpk_eps on one stream).  They share the capture's projection buffer (sequential graph nodes);
+    replays equal the eager loop bitwise, and a second capture of the same loop works too."""
+    from diffpose_amd import utils_diff
+
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(96, seed=19)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    seq = make_seq("uniform", 50, 4)
+    fwd = lambda a, mk, t, c: m(a, mk, t, c)   # noqa: E731  (not a HipGCNdiff: the host-loop path)
+    upd = HipGCNdiff.__new__(HipGCNdiff)
+    utils_diff._init_schedule_only(upd, dev)
+    eager = utils_diff.generalized_steps(x, mask, seq, fwd, _betas(), updater=upd)[0][-1].clone()
+    graphs, outs = [], []
+    for _ in range(2):
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):                       # warm-up: sizes the spare, sets the schedule
+            utils_diff.generalized_steps(x, mask, seq, fwd, _betas(), updater=upd)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        out = torch.empty_like(x)
+        with torch.cuda.graph(g):
+            out.copy_(utils_diff.generalized_steps(x, mask, seq, fwd, _betas(), updater=upd)[0][-1])
+        graphs.append(g)
+        outs.append(out)
+    for _ in range(3):
+        for g, o in zip(graphs, outs):
+            o.zero_()
+            g.replay()
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, eager) for o in outs)
+    del graphs
+    upd.close()
+    m.close()
+
+
+def test_capture_resources_follow_the_graph(dev, monkeypatch):
+    """With DPK_CAPTURE_RELEASE=1 a capture hands its graph a HIP user object: the schedule, the
+    dpk_eps buffer and the step-split flag slot the captured launches read stay held while the graph
+    (or its executable) lives — torch.cuda.CUDAGraph keeps only the executable after capture — and
+    are recycled by the next uncaptured call once it is destroyed.  Probe of the runtime's user-object
+    semantics: released must stay 0 until the graph is gone."""
+    import gc
+
+    monkeypatch.setenv("DPK_CAPTURE_RELEASE", "1")
+    m = _model(dev)
+    x = torch.from_numpy(synthetic_batch(1100, seed=20)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    t = torch.full((1100,), 7.0, device=dev)
+    seq = make_seq("uniform", 50, 4)
+    eager = m.sample(x, seq, _betas()).clone()
+    eager_eps = m(x, mask, t, 0).clone()
+    torch.cuda.synchronize()
+    free0 = m.debug_resources()["free_slots"]
+    out, eo = torch.empty_like(x), torch.empty_like(x)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.sample(x, seq, _betas(), out=out)
+        eo.copy_(m(x, mask, t, 0))
+    r1 = m.debug_resources()
+    print("\nafter capture:", r1)
+    if r1["tracked"] == 0:
+        pytest.skip("the runtime did not retain the user object (resources kept until dpk_destroy)")
+    assert r1["captures"] == 1 and r1["released"] == 0, r1
+    for _ in range(2):
+        out.zero_()
+        eo.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager) and torch.equal(eo, eager_eps)
+    assert m.debug_resources()["released"] == 0
+    del g
+    gc.collect()
+    torch.cuda.synchronize()
+    import time
+
+    for _ in range(100):                  # the runtime may run the destructor on its own thread
+        r2 = m.debug_resources()
+        if r2["released"]:
+            break
+        time.sleep(0.01)
+    print("graph destroyed:", r2)
+    assert r2["released"] == 1, r2
+    assert torch.equal(m.sample(x, seq, _betas()), eager)     # recycles them
+    torch.cuda.synchronize()
+    r3 = m.debug_resources()
+    print("after the next call:", r3)
+    assert r3["captures"] == 0 and r3["free_slots"] >= free0 - 1 and r3["eps_spare_poses"] >= 1100
     m.close()

@@ -55,7 +55,7 @@ def test_sampler_on_other_weights(golden, name, gemm):
     x = torch.from_numpy(g["x"]).cuda()
     mask = torch.ones(1, 1, 17, dtype=torch.bool, device="cuda:0")
     eps = m(x[:8].contiguous(), mask, torch.from_numpy(g["t8"]).cuda(), 0).cpu().numpy()
-    assert np.abs(eps - g["eps"]).max() <= 2e-5
+    assert np.abs(eps - g["eps"]).max() <= ELEM_TOL
     out = m.sample(x, [int(s) for s in g["seq"]], b, mask=mask).cpu().numpy()
     m.close()
     ref, ref64 = g["out"].astype(np.float64), g["out64"]

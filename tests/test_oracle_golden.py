@@ -126,6 +126,39 @@ def test_final_sample(golden, params, graph, name):
     _close(xs[-1].numpy(), g["out"])
 
 
+def test_eta_trajectory_reference_noise(golden, params, graph):
+    """eta > 0 (g11): under the reference's seed the oracle draws the same per-step randn_like and
+    reproduces the reference's trajectory; the stored draws replayed explicitly give the same bits,
+    and ``utils_diff.draw_noise("torch-cpu")`` draws exactly those tensors."""
+    from diffpose_amd.utils_diff import draw_noise
+
+    g = golden("g11_eta.npz")
+    fn = lambda xt, m, tt: O.gcndiff_forward(params, graph, xt, m, tt)  # noqa: E731
+    mask = torch.ones(1, 1, 17, dtype=torch.bool)
+    x = torch.from_numpy(g["x"])
+    seq10 = [int(s) for s in g["seq10"]]
+    torch.manual_seed(int(g["seed10"]))
+    xs, x0s = O.generalized_steps(x, mask, seq10, fn, _betas(51), eta=float(g["eta10"]))
+    _close(torch.stack(xs).numpy(), g["xs10"], 0.0)
+    _close(torch.stack(x0s).numpy(), g["x0s10"], 0.0)
+    torch.manual_seed(int(g["seed10"]))
+    z = draw_noise(x, len(seq10), "torch-cpu")
+    assert torch.equal(z, torch.from_numpy(g["noise10"]))
+    xs_n, _ = O.generalized_steps(x, mask, seq10, fn, _betas(51), eta=float(g["eta10"]), noise=z)
+    _close(xs_n[-1].numpy(), g["xs10"][-1], 0.0)
+    # test_hyber's extra draw before the sampler (runners/diffpose_frame.py:359)
+    torch.manual_seed(int(g["seed_hyber"]))
+    torch.randn_like(x)
+    xs_h, _ = O.generalized_steps(x, mask, seq10, fn, _betas(51), eta=float(g["eta10"]))
+    _close(xs_h[-1].numpy(), g["out_hyber"], 0.0)
+    seq50 = [int(s) for s in g["seq50"]]
+    xs50, _ = O.generalized_steps(x, mask, seq50, fn, _betas(51), eta=float(g["eta50"]),
+                                  noise=torch.from_numpy(g["noise50"]))
+    _close(xs50[-1].numpy(), g["out50"], ATOL)
+    # the noise term is live: another seed's draws give another trajectory
+    assert float(np.abs(g["xs10"][-1] - xs_h[-1].numpy()).max()) > 1e-3
+
+
 def test_schedule_tables():
     for kind in ("linear", "quad", "const", "jsd", "sigmoid"):
         for T in (51, 101):

@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden"))
-    ap.add_argument("--only", default="", help="comma list of fixture groups (g1..g9); default all")
+    ap.add_argument("--only", default="", help="comma list of fixture groups (g1, g2, g34, g5..g9, g11); default all")
     args = ap.parse_args()
     only = set(x for x in args.only.split(",") if x)
 
@@ -309,6 +309,37 @@ def main():
         m7.eval()
         fixture(m7, "g10_synth_seed7.npz", 907, {"weights_seed": 7})
         meta["seed7_weights_sha256"] = state_dict_sha256(sd7)
+
+    # ---------------- G11: eta > 0 with the reference's own per-step randn_like ----------------
+    # generalized_steps draws torch.randn_like(x) once per step (common/utils_diff.py:65); under
+    # torch.manual_seed(s) the K draws are reproducible, so the fixture stores them beside the
+    # trajectory they produced.  test_hyber draws one more randn_like before the sampler
+    # (runners/diffpose_frame.py:359): the "hyber" final is the sampler run after that draw.
+    if want("g11"):
+        def betas51():
+            return torch.from_numpy(get_beta_schedule("linear", beta_start=0.0001, beta_end=0.001,
+                                                      num_diffusion_timesteps=51)).float()
+        x, tgt = synthetic_batch(16, seed=1111)
+        x = torch.from_numpy(x)
+        seq10 = list(range(0, 50, 5))
+        torch.manual_seed(11)
+        xs, x0s = generalized_steps(x, mask, seq10, model, betas51(), eta=0.5)
+        torch.manual_seed(11)
+        noise10 = torch.stack([torch.randn_like(x) for _ in seq10])
+        torch.manual_seed(12)
+        _e = torch.randn_like(x)                       # runners/diffpose_frame.py:359 (unused by the sampler)
+        xs_h, _ = generalized_steps(x, mask, seq10, model, betas51(), eta=0.5)
+        seq50 = list(range(0, 50, 1))
+        torch.manual_seed(13)
+        xs50, _ = generalized_steps(x, mask, seq50, model, betas51(), eta=1.0)
+        torch.manual_seed(13)
+        noise50 = torch.stack([torch.randn_like(x) for _ in seq50])
+        np.savez(os.path.join(args.out, "g11_eta.npz"), x=x.numpy(), targets=tgt, T=51,
+                 seq10=np.array(seq10), eta10=np.float32(0.5), seed10=11, noise10=noise10.numpy(),
+                 xs10=torch.stack(xs).numpy(), x0s10=torch.stack(x0s).numpy(),
+                 seed_hyber=12, out_hyber=xs_h[-1].numpy(),
+                 seq50=np.array(seq50), eta50=np.float32(1.0), seed50=13, noise50=noise50.numpy(),
+                 out50=xs50[-1].numpy())
 
     with open(os.path.join(args.out, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
