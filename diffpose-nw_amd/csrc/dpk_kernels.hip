@@ -193,6 +193,7 @@ using namespace dpk;
 // the schedule it was launched with; the old one is freed once every stream that used it has
 // passed its last launch (an event per stream), or never if a graph was captured with it.
 struct Sched {
+    uint64_t serial = 0;           // unique per schedule built (keys the generic path's loop graphs)
     float* buf = nullptr;          // device: coef, then tps (16-byte aligned)
     float* coef = nullptr;
     float* tps = nullptr;
@@ -1094,6 +1095,8 @@ int dpk_set_schedule(dpk_handle* h, const float* abar, int n_alpha, const int* s
     // an identical schedule keeps its device buffers (and every graph captured with them)
     if (h->sched && h->sched->K == K && h->sched->eta == eta && h->sched->h_coef == c) return DPK_OK;
     Sched* s = new Sched();
+    static uint64_t sched_serial = 0;
+    s->serial = ++sched_serial;
     const size_t tps_off = ((size_t)K * 6 + 3) / 4 * 4;
     hipError_t e = hipMalloc(&s->buf, (tps_off + (size_t)K * NL * D) * 4);
     if (e != hipSuccess) {

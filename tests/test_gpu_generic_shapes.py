@@ -192,3 +192,32 @@ def test_generic_default_mask_and_wide_input_through_c_abi(dev):
                                 n_layers=2, heads=heads)
         assert record_delta(_maxdiff(eps, ref), TOL)
         m.close()
+
+
+def test_generic_loop_graph_matches_direct_launches(dev, monkeypatch):
+    """The generic path records its K-step loop as one hipGraph (keyed by stream scratch, schedule,
+    batch size, mask and seed) and replays it: bitwise the directly launched loop (DPK_GEN_GRAPH=0),
+    across a new key after every change — a per-pose mask, another schedule, a larger batch (the
+    scratch grows, the graphs over the old buffer are dropped), eta > 0 with another seed — and when
+    an earlier key comes back."""
+    hid, heads, layers = 64, 2, 2
+    sd = synthetic_state_dict(hid=hid, n_layers=layers)
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(hid, heads, layers, 17), device=dev)
+    m.load_state_dict(sd)
+    ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    per = torch.ones(40, 1, 17, dtype=torch.bool, device=dev)
+    per[::4, 0, 3:9] = False
+    x40 = _inputs(40, 17, seed=70).to(dev)
+    x90 = _inputs(90, 17, seed=71).to(dev)
+    cases = [(x40, make_seq("uniform", 50, 10), ones, 0.0, 0), (x40, make_seq("uniform", 50, 10), per, 0.0, 0),
+             (x40, make_seq("uniform", 50, 5), ones, 0.0, 0), (x90, make_seq("uniform", 50, 10), ones, 0.0, 0),
+             (x40, make_seq("uniform", 50, 10), ones, 0.0, 0), (x40, make_seq("uniform", 50, 10), ones, 0.4, 3),
+             (x40, make_seq("uniform", 50, 10), ones, 0.4, 4)]
+    for x, seq, mk, eta, seed in cases:
+        monkeypatch.setenv("DPK_GEN_GRAPH", "1")
+        a = m.sample(x, seq, _betas(), eta=eta, mask=mk, seed=seed).clone()
+        a2 = m.sample(x, seq, _betas(), eta=eta, mask=mk, seed=seed).clone()      # replay of the same graph
+        monkeypatch.setenv("DPK_GEN_GRAPH", "0")
+        b = m.sample(x, seq, _betas(), eta=eta, mask=mk, seed=seed)
+        assert torch.equal(a, b) and torch.equal(a2, b), (x.shape[0], len(seq), eta, seed)
+    m.close()

@@ -285,3 +285,25 @@ def test_oracle_on_other_weights(golden, graph, name):
     fn = lambda xt, m, tt: O.gcndiff_forward(P, graph, xt, m, tt)  # noqa: E731
     xs, _ = O.generalized_steps(torch.from_numpy(g["x"]), mask, [int(s) for s in g["seq"]], fn, _betas(int(g["T"])))
     _close(xs[-1].numpy(), g["out"])
+
+
+def test_draw_noise_sources():
+    """utils_diff.draw_noise: "torch" draws randn_like(x) K times on x's device in the reference's
+    order (common/utils_diff.py:65); "philox"/None draw nothing (in-kernel noise); a tensor is
+    checked for shape; anything else raises."""
+    from diffpose_amd.utils_diff import draw_noise
+
+    x = torch.zeros(5, 17, 5)
+    torch.manual_seed(21)
+    z = draw_noise(x, 3, "torch")
+    torch.manual_seed(21)
+    ref = torch.stack([torch.randn_like(x) for _ in range(3)])
+    assert torch.equal(z, ref) and z.dtype == torch.float32
+    g1, g2 = torch.Generator().manual_seed(5), torch.Generator().manual_seed(5)
+    assert torch.equal(draw_noise(x, 2, "torch", generator=g1), draw_noise(x, 2, "torch-cpu", generator=g2))
+    assert draw_noise(x, 3, "philox") is None and draw_noise(x, 3, None) is None
+    assert torch.equal(draw_noise(x, 3, ref), ref)
+    with pytest.raises(ValueError):
+        draw_noise(x, 2, ref)
+    with pytest.raises(ValueError):
+        draw_noise(x, 2, "gaussian")
