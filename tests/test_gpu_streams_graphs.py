@@ -388,14 +388,14 @@ def test_capture_resources_follow_the_graph(dev, monkeypatch):
     mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
     t = torch.full((1100,), 7.0, device=dev)
     seq = make_seq("uniform", 50, 4)
-    eager = m.sample(x, seq, _betas()).clone()
+    eager = m.sample(x, seq, _betas(), mask=mask).clone()
     eager_eps = m(x, mask, t, 0).clone()
     torch.cuda.synchronize()
     free0 = m.debug_resources()["free_slots"]
     out, eo = torch.empty_like(x), torch.empty_like(x)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        m.sample(x, seq, _betas(), out=out)
+    with torch.cuda.graph(g):                     # the same mask object: no mask upload inside the capture
+        m.sample(x, seq, _betas(), mask=mask, out=out)
         eo.copy_(m(x, mask, t, 0))
     r1 = m.debug_resources()
     print("\nafter capture:", r1)
@@ -421,7 +421,7 @@ def test_capture_resources_follow_the_graph(dev, monkeypatch):
         time.sleep(0.01)
     print("graph destroyed:", r2)
     assert r2["released"] == 1, r2
-    assert torch.equal(m.sample(x, seq, _betas()), eager)     # recycles them
+    assert torch.equal(m.sample(x, seq, _betas(), mask=mask), eager)     # recycles them
     torch.cuda.synchronize()
     r3 = m.debug_resources()
     print("after the next call:", r3)

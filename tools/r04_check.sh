@@ -4,7 +4,7 @@
 TAG=${1:-r04}
 O=gpurun_out; mkdir -p $O
 rm -f $O/${TAG}_deltas.jsonl
-DPK_DELTA_LOG=$O/${TAG}_deltas.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 240 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1 || { grep -E "FAILED|Error|assert" $O/${TAG}_gpu_tests.log | head -30; tail -30 $O/${TAG}_gpu_tests.log; exit 1; }
+DPK_DELTA_LOG=$O/${TAG}_deltas.jsonl timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -rP --timeout 240 --timeout-method thread > $O/${TAG}_gpu_tests.log 2>&1 || { grep -E "FAILED|Error|assert" $O/${TAG}_gpu_tests.log | head -30; tail -30 $O/${TAG}_gpu_tests.log; exit 1; }
 grep -E "passed|failed" $O/${TAG}_gpu_tests.log | tail -1
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/${TAG}_smoke.txt 2>&1 || { tail -20 $O/${TAG}_smoke.txt; exit 2; }
 tail -1 $O/${TAG}_smoke.txt
