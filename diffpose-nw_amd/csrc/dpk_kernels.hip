@@ -449,9 +449,10 @@ static int cap_get(dpk_handle* h, hipStream_t st, CapRes** out) {
         }
     CapRes* c = new CapRes();
     c->id = id;
-    // DPK_CAPTURE_RELEASE=1: hand the graph a user object that releases the resources with it
+    // hand the graph a user object that releases the resources with it (DPK_CAPTURE_RELEASE=0: keep them
+    // until dpk_destroy instead)
     const char* env = getenv("DPK_CAPTURE_RELEASE");
-    if (graph && env && atoi(env) == 1) {
+    if (graph && !(env && atoi(env) == 0)) {
         c->refs.fetch_add(1);              // the graph's reference (dropped by cap_release_cb)
         hipUserObject_t obj = nullptr;
         if (hipUserObjectCreate(&obj, c, cap_release_cb, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
@@ -625,21 +626,30 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
     const int gm = h->gemm_mode;
     const char* a16 = gm == 2 ? h->arenabf : h->arena16;
     const dim3 grid(blocks), block(NT);
+#define DPK_LAUNCH3(NS, SP, NZ)                                                                                   \
+    do {                                                                                                        \
+        if (gm == 1) hipLaunchKernelGGL((NS::sample_kernel<MODE, SP, 1, NZ>), grid, block, shmem, st, a, h->arena, a16); \
+        else if (gm == 2) hipLaunchKernelGGL((NS::sample_kernel<MODE, SP, 2, NZ>), grid, block, shmem, st, a, h->arena, a16); \
+        else hipLaunchKernelGGL((NS::sample_kernel<MODE, SP, 0, NZ>), grid, block, shmem, st, a, h->arena, a16);  \
+    } while (0)
 #define DPK_LAUNCH(NS)                                                                                          \
     do {                                                                                                        \
-        if (h->sparse_graph) {                                                                                  \
-            if (gm == 1) hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 1>), grid, block, shmem, st, a, h->arena, a16);  \
-            else if (gm == 2) hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 2>), grid, block, shmem, st, a, h->arena, a16); \
-            else hipLaunchKernelGGL((NS::sample_kernel<MODE, true, 0>), grid, block, shmem, st, a, h->arena, a16);          \
-        } else {                                                                                                \
-            if (gm == 1) hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 1>), grid, block, shmem, st, a, h->arena, a16); \
-            else if (gm == 2) hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 2>), grid, block, shmem, st, a, h->arena, a16); \
-            else hipLaunchKernelGGL((NS::sample_kernel<MODE, false, 0>), grid, block, shmem, st, a, h->arena, a16);         \
+        if constexpr (MODE == M_SAMPLE) {                                                                       \
+            if (a.noise || a.eta != 0.f) {                                                                      \
+                if (a.noise && h->sparse_graph) DPK_LAUNCH3(NS, true, 1);                                       \
+                else if (a.noise) DPK_LAUNCH3(NS, false, 1);                                                    \
+                else if (h->sparse_graph) DPK_LAUNCH3(NS, true, 2);                                             \
+                else DPK_LAUNCH3(NS, false, 2);                                                                 \
+                break;                                                                                          \
+            }                                                                                                   \
         }                                                                                                       \
+        if (h->sparse_graph) DPK_LAUNCH3(NS, true, 0);                                                          \
+        else DPK_LAUNCH3(NS, false, 0);                                                                         \
     } while (0)
     if constexpr (PT == 4) DPK_LAUNCH(dpk);
     else DPK_LAUNCH(dpk2);
 #undef DPK_LAUNCH
+#undef DPK_LAUNCH3
 }
 
 // The sampler over a.N poses.  One 4-pose workgroup per CU per round; a partial last round of r

@@ -375,7 +375,7 @@ def test_capture_of_an_eps_loop_replays_bitwise(dev):
 
 
 def test_capture_resources_follow_the_graph(dev, monkeypatch):
-    """With DPK_CAPTURE_RELEASE=1 a capture hands its graph a HIP user object: the schedule, the
+    """A capture hands its graph a HIP user object (DPK_CAPTURE_RELEASE, default 1): the schedule, the
     dpk_eps buffer and the step-split flag slot the captured launches read stay held while the graph
     (or its executable) lives — torch.cuda.CUDAGraph keeps only the executable after capture — and
     are recycled by the next uncaptured call once it is destroyed.  Probe of the runtime's user-object

@@ -44,6 +44,10 @@ def run(label, hid, heads, layers, force=False, n=1024, k=50):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:          # one shape: generic_bench.py HID HEADS LAYERS [force]  (profiling runs)
+        hid, heads, layers = (int(v) for v in sys.argv[1:4])
+        run(f"hid {hid} / {heads} heads / {layers} layers", hid, heads, layers, force=len(sys.argv) > 4)
+        sys.exit(0)
     run("persistent sampler, hid 96 / 4 heads / 5 layers", 96, 4, 5)
     run("generic path (forced), hid 96 / 4 heads / 5 layers", 96, 4, 5, force=True)
     run("generic path, hid 64 / 2 heads / 2 layers", 64, 2, 2)

@@ -24,7 +24,7 @@ def main():
     rows = []
     for f in glob.glob(os.path.join(a.prof_dir, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "sample_kernel<0, true, 0>" in r["Kernel_Name"]:
+            if "sample_kernel<0, true, 0, 0>" in r["Kernel_Name"]:
                 rows.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6,
                              r["Kernel_Name"]))
     rows.sort()
