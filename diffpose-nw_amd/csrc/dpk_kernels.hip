@@ -64,6 +64,12 @@ __device__ __forceinline__ void tr_stamp() {
 #ifndef DPK_GEMM_HOOK
 #define DPK_GEMM_HOOK(tag)
 #endif
+#ifndef DPK_SPLIT_NOINLINE
+#define DPK_SPLIT_NOINLINE 0   // A/B: the step-split handoff as called functions
+#endif
+#ifndef DPK_ZM0_PHILOX
+#define DPK_ZM0_PHILOX 1   // eta != 0 without a noise buffer stays in the ZM = 0 kernel (the round-3 code)
+#endif
 #ifndef DPK_EXP
 #define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
 #endif
@@ -88,7 +94,6 @@ struct SampleArgs {
     const unsigned* pmask;  // per-pose 17-bit key masks [N] (dpk_set_pose_masks), or null: `mask` for all
     float eta;
     unsigned long long seed;
-    const float* noise;   // [K][N][17][5] caller noise for c1*z (the reference's per-step randn_like), or null: Philox
     int pose_off;         // first pose of this launch (a batch split over two launches, see launch_sampler)
     int num_layers;       // GraAttenLayer + _ResChebGC_diff pairs run (config num_layer, 1..NL)
     // Step-split last round (sample mode, launch_sampler): the last split_n tiles run their K steps
@@ -100,6 +105,9 @@ struct SampleArgs {
     int split_full;
     unsigned* flags;      // [split_n] handoff words: 0 between launches, (token << 2) | state during one
     unsigned token;       // nonzero, per launch (30 bits)
+    // (round 4; after the round-3 fields so their kernel-argument offsets, and the code built around
+    // them, stay as they were)
+    const float* noise;   // [K][N][17][5] caller noise for c1*z (the reference's per-step randn_like), or null
     int* split_stats;     // device counter: second halves that recomputed their first half's steps
     int split_dbg;        // dpk_debug_split: 0 normal; 1 first halves start late; 2 no idle wait
 #if DPK_TRACE
@@ -635,7 +643,7 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
 #define DPK_LAUNCH(NS)                                                                                          \
     do {                                                                                                        \
         if constexpr (MODE == M_SAMPLE) {                                                                       \
-            if (a.noise || a.eta != 0.f) {                                                                      \
+            if (a.noise || (!DPK_ZM0_PHILOX && a.eta != 0.f)) {                                                 \
                 if (a.noise && h->sparse_graph) DPK_LAUNCH3(NS, true, 1);                                       \
                 else if (a.noise) DPK_LAUNCH3(NS, false, 1);                                                    \
                 else if (h->sparse_graph) DPK_LAUNCH3(NS, true, 2);                                             \
