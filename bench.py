@@ -3,9 +3,10 @@
 
 One "step" = one pass of the hot path over one batch: the K=50-step DDIM reverse
 loop (reference common/utils_diff.py:46-68) over B=1024 frames per GPU (config
-human36m_diffpose_uvxyz_cpn eval, H=1), inputs already resident in HBM, plus — for
-N>1 — the RCCL all-gather of the final poses to every rank (frame-sharded, weak
-scaling).  `value` is whole-job poses/s = frames processed by all ranks / time.
+human36m_diffpose_uvxyz_cpn eval, H=1), inputs already resident in HBM, plus — under a
+launcher (N>1, or torch.distributed.run at N=1) — the final MPJPE reduction: per-frame errors of
+each rank's frames (dpk_pose_metrics) and one RCCL all-gather of them, 16 B per frame (frame-sharded,
+weak scaling; the north star's only collective).  `value` is whole-job poses/s = frames processed by all ranks / time.
 
 Launch:
   python bench.py [--gpus N --steps K --warmup W]      N>1: spawns N ranks itself (one process per
@@ -319,14 +320,28 @@ def rank_main(args):
         setup_ms = (time.perf_counter() - t_set) * 1e3
 
     gathered = {}
+    tg_local = torch.from_numpy(tgt_all[lo:hi]).to(dev)
+    if not dry:
+        from diffpose_amd.metrics import pose_errors
+
+    def frame_errors(o):
+        """Per-frame (MPJPE, P-MPJPE) in metres of this rank's frames, [frames, 2] float64: dpk_pose_metrics
+        (hypothesis mean, root-relative, Procrustes, fp64); the cpu-dry stub: MPJPE only."""
+        if dry:
+            v = o.double().view(args.hyp, hi - lo, 17, 5).mean(0)[:, :, 2:]
+            return torch.stack([torch.norm(v - v[:, :1] - tg_local.double(), dim=-1).mean(-1),
+                                torch.full((hi - lo,), float("nan"), dtype=torch.float64)], dim=1)
+        return torch.stack(pose_errors(o, tg_local, args.hyp, root_mode="relative"), dim=1)
 
     def step():
         if dry:
             torch.mul(x, 2.0, out=out)                 # stand-in for the sampler: rank-independent, exact
         else:
             model.sample(x, seq, betas, eta=args.eta, out=out)
-        if use_dist:                                   # the one data-path collective: final poses to every rank
-            gathered["all"] = D.gather_frames(out, B_total, args.hyp)
+        if use_dist:
+            # the one data-path collective, the final MPJPE reduction (north_star): per-frame errors of this
+            # rank's frames, all-gathered (16 B per frame) so every rank holds the whole job's MPJPE
+            gathered["fe"] = D.gather_frames(frame_errors(out), B_total, 1)
 
     def measure(gemm):
         """Time exactly args.steps steps (barrier + sync both sides, max over ranks) in one GEMM mode."""
@@ -405,16 +420,19 @@ def rank_main(args):
         lst = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(lst, t)
         per_rank_ms = [round(float(v.item()), 4) for v in lst]
-        # the all-gather alone, same barrier/sync bracket, max over ranks
+        # the step's all-gather alone (per-frame errors, 16 B per frame), same barrier/sync bracket, max over ranks
+        fe_local = frame_errors(out)
         dist.barrier()
         sync()
         t0 = time.perf_counter()
         n_ag = 20
         for _ in range(n_ag):
-            full = D.gather_frames(out, B_total, args.hyp)
+            D.gather_frames(fe_local, B_total, 1)
         sync()
         dist.barrier()
         allgather_ms = D.max_over_ranks(time.perf_counter() - t0, device=dev) / n_ag * 1e3
+        # the final poses reassembled once (not part of the step): every shard where shard_rows puts it
+        full = D.gather_frames(out, B_total, args.hyp)
         if dry:   # the stub is exact, so the reassembled batch must equal the stub over the whole batch
             expect = torch.from_numpy(repeat_hypotheses(x_all, args.hyp)) * 2.0
             reassembly = bool(torch.equal(full.cpu(), expect))
@@ -426,33 +444,33 @@ def rank_main(args):
     # ---- the final MPJPE reduction (runners/diffpose_frame.py:382-387): per-frame (MPJPE, P-MPJPE) of this
     #      rank's frames (dpk_pose_metrics: hypothesis mean, root-relative, Procrustes, fp64), then one
     #      all-gather of those 16 B per frame; every rank ends with the job's MPJPE.  Once, after the timed steps.
-    tg_local = torch.from_numpy(tgt_all[lo:hi]).to(dev)
-    if not dry:      # one untimed pass first (first launches in this process: the metrics kernel, torch's cat)
-        from diffpose_amd.metrics import pose_errors
-
-        torch.stack(pose_errors(out, tg_local, args.hyp, root_mode="relative"), dim=1)
+    frame_errors(out)      # untimed first (first launches in this process: the metrics kernel, torch's cat)
     if use_dist:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    if dry:    # no HIP metrics kernel on CPU: MPJPE of the stub output, P-MPJPE not computed
-        o = out.double().view(args.hyp, hi - lo, 17, 5).mean(0)[:, :, 2:]
-        fe = torch.stack([torch.norm(o - o[:, :1] - tg_local.double(), dim=-1).mean(-1),
-                          torch.full((hi - lo,), float("nan"), dtype=torch.float64)], dim=1)
-    else:
-        fe = torch.stack(pose_errors(out, tg_local, args.hyp, root_mode="relative"), dim=1)
+    fe = frame_errors(out)
     if use_dist:
         fe = D.gather_frames(fe, B_total, 1)
+        # the timed steps' own reduction of the same output gave the same numbers
+        g = gathered["fe"]
+        eq = bool(((fe == g) | (torch.isnan(fe) & torch.isnan(g))).all())      # the dry stub's P-MPJPE is NaN
+        same = torch.tensor([1 if eq else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
     sync()
     reduce_s = time.perf_counter() - t0
     if use_dist:
         reduce_s = D.max_over_ranks(reduce_s, device=dev)
     fe_h = fe.cpu().numpy()
+    if use_dist and not bool(same.item()):
+        print("bench: the steps' gathered per-frame errors differ from the final reduction's", file=sys.stderr)
+        return 3
     mpjpe_line = {"p1_mm": round(float(fe_h[:, 0].mean()) * 1000.0, 6),
                   "p2_mm": None if dry else round(float(fe_h[:, 1].mean()) * 1000.0, 6),
                   "frames": int(fe_h.shape[0]), "reduce_ms": round(reduce_s * 1e3, 4),
                   "how": ("per-frame (MPJPE, P-MPJPE) on each rank's frames (dpk_pose_metrics, fp64), " +
-                          ("one RCCL all_gather of 16 B per frame" if use_dist else "one rank, no collective")),
+                          ("one all_gather of 16 B per frame, inside every timed step" if use_dist
+                           else "one rank, no collective; after the timed steps")),
                   "targets": "synthetic (seeded), root-relative"}
     out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0 and not dry) else None
     variants = {}
@@ -484,7 +502,8 @@ def rank_main(args):
                                f"T={args.T}), eta={args.eta}",
                    "baseline_config": args.config, "frames_total": B_total, "frames_per_gpu": hi - lo,
                    "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
-                   "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of final poses" if use_dist else ""),
+                   "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of per-frame errors (the final MPJPE "
+                                                                          "reduction)" if use_dist else ""),
                    "hipgraph": bool(args.graph), "gemm": args.gemm},
         "per_rank_ms": per_rank_ms,
         "setup_ms": None if setup_ms is None else round(setup_ms, 4),
