@@ -452,13 +452,13 @@ def rank_main(args):
     fe = frame_errors(out)
     if use_dist:
         fe = D.gather_frames(fe, B_total, 1)
-        # the timed steps' own reduction of the same output gave the same numbers
+    sync()
+    reduce_s = time.perf_counter() - t0
+    if use_dist:   # the timed steps' own reduction of the same output gave the same numbers
         g = gathered["fe"]
         eq = bool(((fe == g) | (torch.isnan(fe) & torch.isnan(g))).all())      # the dry stub's P-MPJPE is NaN
         same = torch.tensor([1 if eq else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(same, op=dist.ReduceOp.MIN)
-    sync()
-    reduce_s = time.perf_counter() - t0
     if use_dist:
         reduce_s = D.max_over_ranks(reduce_s, device=dev)
     fe_h = fe.cpu().numpy()
