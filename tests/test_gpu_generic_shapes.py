@@ -221,3 +221,26 @@ def test_generic_loop_graph_matches_direct_launches(dev, monkeypatch):
         b = m.sample(x, seq, _betas(), eta=eta, mask=mk, seed=seed)
         assert torch.equal(a, b) and torch.equal(a2, b), (x.shape[0], len(seq), eta, seed)
     m.close()
+
+
+def test_generic_eta_with_caller_noise_vs_oracle(dev):
+    """eta > 0 on the generic path with the caller's draws (dpk_sample_noise; the launches go
+    straight to the stream, the recorded loop only covers eta's counter-based draws): the K=10
+    trajectory equals the oracle's run on the same draws within the bar."""
+    from oracle import gcndiff_oracle as O
+
+    hid, heads, layers = 64, 2, 2
+    sd = synthetic_state_dict(hid=hid, n_layers=layers)
+    adj = adj_mx_from_edges()
+    m = HipGCNdiff(adj, _cfg(hid, heads, layers, 17), device=dev)
+    m.load_state_dict(sd)
+    x = _inputs(20, 17, seed=81)
+    seq = make_seq("uniform", 50, 10)
+    z = torch.randn((10,) + tuple(x.shape), generator=torch.Generator().manual_seed(8))
+    ones = torch.ones(1, 1, 17, dtype=torch.bool)
+    xs, _ = m.sample(x.to(dev), seq, _betas(), eta=0.6, mask=ones.to(dev), trajectory=True, noise=z.to(dev))
+    P = O.params_to_torch(sd)
+    fwd = lambda a, mk, t: O.gcndiff_forward(P, torch.from_numpy(adj), a, mk, t, n_layers=layers, heads=heads)  # noqa: E731
+    rxs, _ = O.generalized_steps(x, ones, seq, fwd, _betas(), eta=0.6, noise=z)
+    assert record_delta(_maxdiff(xs, torch.stack(rxs)), TOL)
+    m.close()
