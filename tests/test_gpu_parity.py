@@ -286,6 +286,11 @@ def test_step_split_with_noise_and_fallback(model, mask):
         assert 0 <= model.debug_split(0, read=True) <= 19
         assert torch.equal(model.sample(xt, seq, _betas(51), mask=mask), ref0)   # back to normal: flags clean
         assert model.debug_split(0, read=True) == 0
+        # the 2-pose tail round (second launch at pose offset 1,024) reads the same noise rows
+        model.set_tail_plan("two_pose")
+        out1 = model.sample(xt, seq, _betas(51), eta=0.7, mask=mask, noise=noise)
+        assert torch.equal(out1[:1024], ref[:1024])
+        assert record_delta(_maxdiff(out1, ref), TRAJ_TOL)
     finally:
         model.debug_split(0)
         model.set_tail_plan("step_split")
