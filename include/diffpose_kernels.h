@@ -37,7 +37,9 @@
  *     (after one device-wide wait).  The first captured dpk_eps of a capture takes the handle's
  *     spare projection buffer, which every uncaptured dpk_eps of at least N poses sizes: make one
  *     with the capture's largest N before it (else DPK_E_STATE).  Replays of one executable graph
- *     must not overlap each other (HIP orders launches of the same graph exec).
+ *     must not overlap each other (HIP orders launches of the same graph exec), and neither may
+ *     two executable instances of one captured graph (they share its projection buffer and flag
+ *     slot): capture again for a second concurrent instance.
  */
 #ifndef DIFFPOSE_KERNELS_H
 #define DIFFPOSE_KERNELS_H
