@@ -406,6 +406,9 @@ def rank_main(args):
                 if key in tr:
                     roof["traffic"] = tr[key]["hbm_bytes_per_launch"]
                     roof["traffic_source"] = tr[key]["source"]
+                    if "mfma_busy" in tr[key]:      # the executed-work figure beside frac
+                        roof["mfma_busy"] = tr[key]["mfma_busy"]
+                        roof["mfma_busy_source"] = tr[key]["mfma_busy_source"]
             except (OSError, ValueError, KeyError):
                 pass
         return roof
