@@ -24,9 +24,9 @@ Also reported on the same JSON line:
                 pose-step × poses × K ÷ its average launch duration, measured with HIP events
                 around that kernel on the stream it is launched on) vs the fp32 MFMA peak;
   cpu_baseline  the golden-pinned oracle (torch CPU, the reference's op sequence) timed on
-                this host's cores on the first --cpu-frames frames of the same batch (rank 0,
-                N=1 only), best of --cpu-repeats after a warm-up call, at the host threads the
-                job is allotted (OMP_NUM_THREADS; --cpu-threads adds legs);
+                this host's cores on the same batch (rank 0, N=1 only; all of it up to 1024 rows,
+                --cpu-frames to change), best of --cpu-repeats after a warm-up call, at the host
+                threads the job is allotted (OMP_NUM_THREADS; --cpu-threads adds legs);
   parity        MPJPE (mm) of the HIP result vs the oracle on those frames, and max |diff|;
   mpjpe         the job's MPJPE / P-MPJPE over all frames by the final reduction: per-frame errors on
                 every rank (dpk_pose_metrics) and one all-gather of 16 B per frame (after the timed steps);
@@ -87,7 +87,9 @@ def parse(argv=None):
     ap.add_argument("--T", type=int, default=None, help="diffusion.num_diffusion_timesteps")
     ap.add_argument("--eta", type=float, default=0.0)
     ap.add_argument("--graph", action="store_true", default=None, help="replay the step from a captured hipGraph")
-    ap.add_argument("--cpu-frames", type=int, default=128)
+    ap.add_argument("--cpu-frames", type=int, default=None,
+                    help="frames of the CPU baseline and parity sample (default: rank 0's whole batch, at most "
+                         "1024 rows, i.e. 1024 // H frames)")
     ap.add_argument("--cpu-repeats", type=int, default=3)
     ap.add_argument("--cpu-threads", type=str, default=None,
                     help="comma-separated thread counts for the CPU baseline legs (default: the box's CPU share, "
@@ -210,7 +212,7 @@ def cpu_baseline(args, x_all, seq, betas, K, hyp):
     phys = physical_cores(cpus)
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or phys
     share = max(1, min(share, len(cpus)))
-    n_cpu = min(args.cpu_frames, x_all.shape[0])
+    n_cpu = min(args.cpu_frames if args.cpu_frames else max(1, 1024 // hyp), x_all.shape[0])
     xc = torch.from_numpy(repeat_hypotheses(x_all[:n_cpu], hyp))
     P = O.params_to_torch(synthetic_state_dict())
     adj = O.adjacency()
@@ -338,10 +340,11 @@ def rank_main(args):
             torch.mul(x, 2.0, out=out)                 # stand-in for the sampler: rank-independent, exact
         else:
             model.sample(x, seq, betas, eta=args.eta, out=out)
-        if use_dist:
-            # the one data-path collective, the final MPJPE reduction (north_star): per-frame errors of this
-            # rank's frames, all-gathered (16 B per frame) so every rank holds the whole job's MPJPE
-            gathered["fe"] = D.gather_frames(frame_errors(out), B_total, 1)
+        # the final MPJPE reduction (north_star) at every N, N=1 included, so every point of the scaling
+        # sweep times the same work: per-frame errors of this rank's frames (dpk_pose_metrics), and under
+        # a launcher the one data-path collective, their all-gather (16 B per frame)
+        fe_step = frame_errors(out)
+        gathered["fe"] = D.gather_frames(fe_step, B_total, 1) if use_dist else fe_step
 
     def measure(gemm):
         """Time exactly args.steps steps (barrier + sync both sides, max over ranks) in one GEMM mode."""
@@ -457,15 +460,16 @@ def rank_main(args):
         fe = D.gather_frames(fe, B_total, 1)
     sync()
     reduce_s = time.perf_counter() - t0
-    if use_dist:   # the timed steps' own reduction of the same output gave the same numbers
-        g = gathered["fe"]
-        eq = bool(((fe == g) | (torch.isnan(fe) & torch.isnan(g))).all())      # the dry stub's P-MPJPE is NaN
-        same = torch.tensor([1 if eq else 0], dtype=torch.int32, device=dev)
+    # the timed steps' own reduction of the same output gave the same numbers
+    g = gathered["fe"]
+    eq = bool(((fe == g) | (torch.isnan(fe) & torch.isnan(g))).all())      # the dry stub's P-MPJPE is NaN
+    same = torch.tensor([1 if eq else 0], dtype=torch.int32, device=dev)
+    if use_dist:
         dist.all_reduce(same, op=dist.ReduceOp.MIN)
     if use_dist:
         reduce_s = D.max_over_ranks(reduce_s, device=dev)
     fe_h = fe.cpu().numpy()
-    if use_dist and not bool(same.item()):
+    if not bool(same.item()):
         print("bench: the steps' gathered per-frame errors differ from the final reduction's", file=sys.stderr)
         return 3
     mpjpe_line = {"p1_mm": round(float(fe_h[:, 0].mean()) * 1000.0, 6),
@@ -473,7 +477,7 @@ def rank_main(args):
                   "frames": int(fe_h.shape[0]), "reduce_ms": round(reduce_s * 1e3, 4),
                   "how": ("per-frame (MPJPE, P-MPJPE) on each rank's frames (dpk_pose_metrics, fp64), " +
                           ("one all_gather of 16 B per frame, inside every timed step" if use_dist
-                           else "one rank, no collective; after the timed steps")),
+                           else "one rank, no collective; inside every timed step (the same work as at N>1)")),
                   "targets": "synthetic (seeded), root-relative"}
     out_main = out.detach().cpu().numpy() if (world == 1 and rank == 0 and not dry) else None
     variants = {}
@@ -505,8 +509,9 @@ def rank_main(args):
                                f"T={args.T}), eta={args.eta}",
                    "baseline_config": args.config, "frames_total": B_total, "frames_per_gpu": hi - lo,
                    "hypotheses": args.hyp, "rows_per_gpu": rows, "K": K,
-                   "parallelism": f"dp{world} frame-sharded" + (" + RCCL all_gather of per-frame errors (the final MPJPE "
-                                                                          "reduction)" if use_dist else ""),
+                   "parallelism": f"dp{world} frame-sharded; every step = sampler + per-frame MPJPE/P-MPJPE "
+                                  f"(dpk_pose_metrics)" + (" + RCCL all_gather of the per-frame errors (the final "
+                                                           "MPJPE reduction)" if use_dist else ""),
                    "hipgraph": bool(args.graph), "gemm": args.gemm},
         "per_rank_ms": per_rank_ms,
         "setup_ms": None if setup_ms is None else round(setup_ms, 4),

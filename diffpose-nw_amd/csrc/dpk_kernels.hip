@@ -241,6 +241,14 @@ struct CapRes {
     std::vector<Sched*> scheds;
     std::vector<EpsBuf> eps;                   // per capturing stream
     std::vector<std::pair<hipStream_t, int>> slots;   // flag slot per capturing stream
+    // generic-shape path: the activation scratch of each capturing stream (taken from the model's
+    // spare, which uncaptured generic calls size; dpk_generic.inc gen_scratch_cap)
+    struct GenBuf {
+        hipStream_t st;
+        float* p;
+        size_t cap;   // floats
+    };
+    std::vector<GenBuf> gen;
 };
 static void cap_release_cb(void* p) {
     CapRes* c = static_cast<CapRes*>(p);
@@ -249,6 +257,8 @@ static void cap_release_cb(void* p) {
 }
 
 struct GenModel;   // dpk_generic.inc: the forward for model shapes other than the compiled one
+struct dpk_handle;
+static void gen_spare_put(dpk_handle* h, float* p, size_t cap);   // dpk_generic.inc
 
 struct dpk_handle {
     int device = 0;
@@ -480,6 +490,18 @@ static int cap_get(dpk_handle* h, hipStream_t st, CapRes** out) {
 
 static void slot_put(dpk_handle* h, int slot) { h->slot_free.push_back(slot); }
 
+// Wait for the device in relaxed capture mode: a thread capturing in global mode (torch.cuda.graph's
+// default) would otherwise see this potentially unsafe call invalidate its capture.  false (error
+// cleared) if the runtime refuses the sync, e.g. while a stream of the device is capturing.
+static bool drain_relaxed() {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    const bool exch = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+    const hipError_t se = hipDeviceSynchronize();
+    if (exch) (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (se != hipSuccess) (void)hipGetLastError();
+    return se == hipSuccess;
+}
+
 // Uncaptured calls only: recycle the resources of captures whose graphs are gone.  The release
 // callback may run while a replay is still in flight on some stream, so the device is drained once
 // before anything is reused (graph destruction is rare; nothing waits otherwise).
@@ -487,10 +509,7 @@ static void cap_sweep(dpk_handle* h) {
     bool any = false;
     for (CapRes* c : h->caps) any = any || (c->tracked && c->released.load());
     if (!any) return;
-    if (hipDeviceSynchronize() != hipSuccess) {    // e.g. another thread is capturing: try again later
-        (void)hipGetLastError();
-        return;
-    }
+    if (!drain_relaxed()) return;     // a stream of the device is capturing: the resources wait for a later call
     std::vector<CapRes*> keep;
     for (CapRes* c : h->caps) {
         if (!(c->tracked && c->released.load())) {
@@ -507,6 +526,7 @@ static void cap_sweep(dpk_handle* h) {
             }
         }
         for (auto& s : c->slots) slot_put(h, s.second);
+        for (auto& gb : c->gen) gen_spare_put(h, gb.p, gb.cap);
         if (c->refs.fetch_sub(1) == 1) delete c;
     }
     h->caps.swap(keep);
@@ -807,6 +827,7 @@ void dpk_destroy(dpk_handle* h) {
     if (h->eps_spare.p) (void)hipFree(h->eps_spare.p);
     for (CapRes* c : h->caps) {
         for (auto& e : c->eps) (void)hipFree(e.p);
+        for (auto& gb : c->gen) (void)hipFree(gb.p);
         // a graph still alive keeps the CapRes object (its callback touches only that)
         if (c->refs.fetch_sub(1) == 1) delete c;
     }
@@ -1436,9 +1457,9 @@ int dpk_debug_resources(dpk_handle* h, int* out, int n) {
         tracked += c->tracked ? 1 : 0;
         released += (c->tracked && c->released.load()) ? 1 : 0;
     }
-    const int v[6] = {(int)h->caps.size(), tracked, released, (int)h->slot_free.size(), retired,
-                      h->eps_spare.cap};
-    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    const int v[8] = {(int)h->caps.size(), tracked, released, (int)h->slot_free.size(), retired,
+                      h->eps_spare.cap, gen_graph_count(h->gen), gen_spare_mib(h->gen)};
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
     return DPK_OK;
 }
 

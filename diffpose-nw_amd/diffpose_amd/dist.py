@@ -5,13 +5,13 @@ The reference runs one GPU (``torch.nn.DataParallel`` over a single device,
 (no BatchNorm, no cross-pose op), so N GPUs each take a contiguous range of frames —
 with all ``test_times`` hypotheses of those frames, keeping the hypothesis mean local
 (``runners/diffpose_frame.py:342``, ``:382``) — and run the sampler on it with no
-data-path collective.  The only exchanges are
+data-path collective.  The one exchange is
 
-* ``gather_frames``: one ``all_gather_into_tensor`` of the final poses (hypothesis-major
-  layout restored), for consumers that need the whole batch, and
-* ``allreduce_sums``: one all-reduce of per-rank metric sums (MPJPE / P-MPJPE numerators
-  and pose counts), the distributed form of the ``AverageMeter`` updates at
-  ``runners/diffpose_frame.py:386-387``.
+* ``gather_frames``: one ``all_gather_into_tensor`` of per-frame rows (hypothesis-major layout
+  restored).  The evaluation gathers each frame's (MPJPE, P-MPJPE), 16 B per frame
+  (``runner.Diffpose.test_hyber``, ``bench.py``), so every rank books the whole batch with the
+  reference's accounting (``common/utils.py:136-150``); per-rank metric sums cannot reproduce its
+  P-MPJPE booking, which is why no sum all-reduce is used.
 
 One process per GPU (``torch.distributed`` with backend "nccl" = RCCL on ROCm, "gloo" on
 CPU for tests).  Ragged shards are padded to the largest shard for the collective.
@@ -69,14 +69,6 @@ def gather_frames(local: torch.Tensor, n_frames: int, hyp: int, out: torch.Tenso
         rlo, rhi = shard_frames(n_frames, world, r)
         resv[:, rlo:rhi] = buf[r, :, : rhi - rlo]
     return res
-
-
-def allreduce_sums(values, device=None, group=None):
-    """Sum a short vector of float64 metric accumulators over ranks (e.g. [sum_p1, sum_p2, count])."""
-    t = torch.as_tensor(values, dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return t
 
 
 def max_over_ranks(seconds: float, device=None, group=None) -> float:

@@ -224,9 +224,10 @@ class _HipModel:
 
     def debug_resources(self) -> dict:
         """Test hook (dpk_debug_resources): capture-owned resources and free flag slots."""
-        buf = (ctypes.c_int * 6)()
-        _lib.check(self._h, "dpk_debug_resources", _lib.lib().dpk_debug_resources(self._h, buf, 6))
-        keys = ("captures", "tracked", "released", "free_slots", "retired_schedules", "eps_spare_poses")
+        buf = (ctypes.c_int * 8)()
+        _lib.check(self._h, "dpk_debug_resources", _lib.lib().dpk_debug_resources(self._h, buf, 8))
+        keys = ("captures", "tracked", "released", "free_slots", "retired_schedules", "eps_spare_poses",
+                "generic_loop_graphs", "generic_spare_mib")
         return dict(zip(keys, list(buf)))
 
     def profile(self, enable: bool = True) -> None:

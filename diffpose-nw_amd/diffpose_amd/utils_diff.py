@@ -78,8 +78,7 @@ def generalized_steps(x, src_mask, seq, model, b, **kwargs):
         # generic callable: host loop, HIP DDIM update
         upd = kwargs.get("updater")
         if upd is None:
-            upd = HipGCNdiff.__new__(HipGCNdiff)
-            _init_schedule_only(upd, x.device)
+            upd = schedule_handle(x.device)
         upd.set_schedule(seq, b, eta)
         n = x.size(0)
         xs, x0s = [x], []
@@ -90,6 +89,27 @@ def generalized_steps(x, src_mask, seq, model, b, **kwargs):
             x0s.append(x0)
             xs.append(xn)
         return xs, x0s
+
+
+# One schedule-only DDIM handle per (device, thread), reused by every generic-callable call: the
+# reference's sampler allocates nothing persistent (common/utils_diff.py:46-68), so neither should
+# a call here (a handle costs dpk_create, device buffers and a schedule upload).  A handle serves one
+# thread (include/diffpose_kernels.h), hence the thread in the key.
+_SCHED_HANDLES: dict = {}
+
+
+def schedule_handle(device) -> HipGCNdiff:
+    """The cached schedule-only handle of ``device`` for the calling thread (created on first use)."""
+    import threading
+
+    dev = torch.device(device)
+    key = (dev.type, dev.index or 0, threading.get_ident())
+    upd = _SCHED_HANDLES.get(key)
+    if upd is None:
+        upd = HipGCNdiff.__new__(HipGCNdiff)
+        _init_schedule_only(upd, dev)
+        _SCHED_HANDLES[key] = upd
+    return upd
 
 
 def _init_schedule_only(obj: HipGCNdiff, device) -> None:

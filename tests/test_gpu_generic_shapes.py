@@ -147,16 +147,85 @@ def test_generic_gcnpose_vs_oracle(dev):
     m.close()
 
 
-def test_generic_path_refuses_capture(dev):
+def test_generic_path_under_caller_capture(dev):
+    """A caller's torch.cuda.graph around the generic path (config 5's pattern, common/utils_diff.py:46-68
+    called from runners/diffpose_frame.py:365): the launches are recorded into the caller's graph on the
+    capture's own scratch (the model's spare, sized by the uncaptured warm-up), and every replay is
+    bitwise the eager result, for dpk_sample (K=4), dpk_eps, a captured loop of two samples on one
+    stream, and GCNpose; the scratch returns to the spare when the graph is destroyed."""
+    hid, heads, layers = 64, 2, 2
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(hid, heads, layers, 17), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=hid, n_layers=layers))
+    ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    x = _inputs(24, 17, seed=70).to(dev)
+    t = (torch.arange(24, dtype=torch.float32) * 2.0).to(dev)
+    seq = make_seq("uniform", 50, 4)
+    eager = m.sample(x, seq, _betas(), mask=ones).clone()
+    eps_eager = m(x, ones, t, 0).clone()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):                 # warm-up on the capture's side stream (torch's pattern)
+        m.sample(x, seq, _betas(), mask=ones)
+        m(x, ones, t, 0)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    out = torch.empty_like(x)
+    out2 = torch.empty_like(x)
+    eps = torch.empty_like(x)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.sample(x, seq, _betas(), mask=ones, out=out)
+        m.sample(out, seq, _betas(), mask=ones, out=out2)      # a captured loop: the second shares the scratch
+        eps.copy_(m(x, ones, t, 0))
+    assert m.debug_resources()["captures"] >= 1
+    second = m.sample(eager, seq, _betas(), mask=ones).clone()
+    for _ in range(2):
+        out.zero_()
+        out2.zero_()
+        eps.zero_()
+        g.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(out, eager) and torch.equal(out2, second) and torch.equal(eps, eps_eager)
+    del g
+    import gc
+
+    gc.collect()
+    torch.cuda.synchronize(dev)
+    m.sample(x, seq, _betas(), mask=ones)       # an uncaptured call recycles the capture's resources
+    r = m.debug_resources()
+    assert r["released"] == 0 and r["generic_spare_mib"] >= 0
+    m.close()
+
+
+def test_generic_capture_without_warmup_is_refused(dev):
     m = HipGCNdiff(adj_mx_from_edges(), _cfg(64, 2, 1, 17), device=dev)
     m.load_state_dict(synthetic_state_dict(hid=64, n_layers=1))
     x = _inputs(8, 17, seed=70).to(dev)
     seq = make_seq("uniform", 50, 2)
-    m.sample(x, seq, _betas())
+    m.set_schedule(seq, _betas())
     g = torch.cuda.CUDAGraph()
     with pytest.raises(Exception):
         with torch.cuda.graph(g):
-            m.sample(x, seq, _betas())
+            m.sample(x, seq, _betas())          # no uncaptured call has sized the spare
+    m.close()
+
+
+def test_generic_eta0_seed_shares_one_loop_graph(dev):
+    """advisor r04: at eta = 0 the seed is not read, so calls that differ only in seed (test_hyber
+    passes seed + i per batch) replay one recorded loop instead of recording one each; at eta > 0
+    the seed keys the graph (the counter-based draws depend on it)."""
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(64, 2, 1, 17), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=64, n_layers=1))
+    ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    x = _inputs(16, 17, seed=72).to(dev)
+    seq = make_seq("uniform", 50, 5)
+    a = m.sample(x, seq, _betas(), mask=ones, seed=1).clone()
+    n0 = m.debug_resources()["generic_loop_graphs"]
+    for sd in range(2, 12):
+        assert torch.equal(m.sample(x, seq, _betas(), mask=ones, seed=sd), a)
+    assert m.debug_resources()["generic_loop_graphs"] == n0 == 1
+    m.sample(x, seq, _betas(), mask=ones, eta=0.5, seed=1)
+    m.sample(x, seq, _betas(), mask=ones, eta=0.5, seed=2)
+    assert m.debug_resources()["generic_loop_graphs"] == 3
     m.close()
 
 

@@ -121,6 +121,16 @@ def test_generic_callable_path(model, mask):
     gen_xs, gen_x0s = utils_diff.generalized_steps(x, mask, seq, lambda a, m, t, c: model(a, m, t, c), _betas(51).cuda())
     assert _maxdiff(torch.stack(gen_xs), torch.stack(ref_xs)) <= 1e-6
     assert _maxdiff(torch.stack(gen_x0s), torch.stack(ref_x0s)) <= 1e-6
+    # the schedule-only DDIM handle is created once per device and reused: a second call (another
+    # schedule) allocates no new handle, and the first call's results come back unchanged after it
+    h1 = utils_diff.schedule_handle(x.device)
+    n_handles = len(utils_diff._SCHED_HANDLES)
+    seq2 = make_seq("uniform", 50, 5)
+    utils_diff.generalized_steps(x, mask, seq2, lambda a, m, t, c: model(a, m, t, c), _betas(51).cuda())
+    again_xs, _ = utils_diff.generalized_steps(x, mask, seq, lambda a, m, t, c: model(a, m, t, c), _betas(51).cuda())
+    assert utils_diff.schedule_handle(x.device) is h1 and len(utils_diff._SCHED_HANDLES) == n_handles
+    assert h1._h.value == utils_diff.schedule_handle(x.device)._h.value
+    assert torch.equal(torch.stack(again_xs), torch.stack(gen_xs))
 
 
 @pytest.mark.parametrize("n", [1, 3, 5, 67])

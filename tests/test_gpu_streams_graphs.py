@@ -427,3 +427,79 @@ def test_capture_resources_follow_the_graph(dev, monkeypatch):
     print("after the next call:", r3)
     assert r3["captures"] == 0 and r3["free_slots"] >= free0 - 1 and r3["eps_spare_poses"] >= 1100
     m.close()
+
+
+def test_sweep_while_another_thread_captures(dev, monkeypatch):
+    """advisor r04: handle B's uncaptured dpk_sample recycles a released capture's resources (a device
+    drain, cap_sweep) while thread A holds a global-mode capture open (torch.cuda.graph's default) on
+    handle A.  The drain runs in relaxed capture mode, or is put off to a later call when the runtime
+    refuses it: A's capture must complete and replay bitwise, and B's launch gives the eager result."""
+    import gc
+    import threading
+    import time
+
+    monkeypatch.setenv("DPK_CAPTURE_RELEASE", "1")
+    mA, mB = _model(dev), _model(dev)
+    x = torch.from_numpy(synthetic_batch(64, seed=23)[0]).to(dev)
+    mask = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    seq = make_seq("uniform", 50, 4)
+    eager = mA.sample(x, seq, _betas(), mask=mask).clone()
+    assert torch.equal(mB.sample(x, seq, _betas(), mask=mask), eager)
+    # B: a capture whose graph is destroyed, so B's next uncaptured call has a release to sweep
+    outB = torch.empty_like(x)
+    gB = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gB):
+        mB.sample(x, seq, _betas(), mask=mask, out=outB)
+    if mB.debug_resources()["tracked"] == 0:
+        pytest.skip("the runtime did not retain the user object (nothing is swept)")
+    del gB
+    gc.collect()
+    torch.cuda.synchronize()
+    for _ in range(100):
+        if mB.debug_resources()["released"]:
+            break
+        time.sleep(0.01)
+    assert mB.debug_resources()["released"] == 1
+    # A: warm up on the capture's side stream, then hold the capture open while B sweeps
+    sA = torch.cuda.Stream(device=dev)
+    sA.wait_stream(torch.cuda.current_stream(dev))
+    outA = torch.empty_like(x)
+    with torch.cuda.stream(sA):
+        mA.sample(x, seq, _betas(), mask=mask, out=outA)
+    torch.cuda.current_stream(dev).wait_stream(sA)
+    torch.cuda.synchronize()
+    sB = torch.cuda.Stream(device=dev)
+    resB = torch.empty_like(x)
+    opened, done = threading.Event(), threading.Event()
+    errs = []
+
+    def thread_b():
+        try:
+            assert opened.wait(60)
+            with torch.cuda.device(dev), torch.cuda.stream(sB):
+                mB.sample(x, seq, _betas(), mask=mask, out=resB)    # preallocated: no allocator call
+        except Exception as e:  # surfaced below
+            errs.append(repr(e))
+        finally:
+            done.set()
+
+    tb = threading.Thread(target=thread_b)
+    tb.start()
+    gA = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gA):
+        mA.sample(x, seq, _betas(), mask=mask, out=outA)
+        opened.set()
+        assert done.wait(120)
+    tb.join(60)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    assert torch.equal(resB, eager)
+    outA.zero_()
+    gA.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(outA, eager)
+    mB.sample(x, seq, _betas(), mask=mask)       # a later call recycles the release if the first was refused
+    assert mB.debug_resources()["released"] == 0
+    del gA
+    mA.close()
+    mB.close()
