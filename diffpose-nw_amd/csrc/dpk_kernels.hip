@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <atomic>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -359,40 +360,38 @@ static inline uint16_t bf16_rne(float v) {
 }
 static inline float bf16_to_f32(uint16_t b) { return __builtin_bit_cast(float, (uint32_t)b << 16); }
 
-// Split W_eff * W16_SCALE into hi + lo 16x16x32 B fragments [NC][KB32][hi|lo][64][8]:
-// BF = false: hi = fp16(v) (RNE), lo = fp16(v - hi); v - hi is exact in fp32 (Sterbenz).
-// BF = true:  the same with bf16 (gemm mode 2 reads only hi).
+// Split W_eff * W16_SCALE into 16x16x32 B fragments for the half-width-operand GEMMs (gemmh_pass):
+// lane l holds column n = ct*16 + (l&15) at the 8 k of its lane group g = l>>4 in the order
+// 4g..4g+3, 16+4g..16+4g+3 of the 32-block (the A fragments' order: two fp32 16x16x4 fragments).
+// BF = false (gemm mode 1, f16x3): blocks [NC][KB32][hi 1 KiB | lo 1 KiB], hi = fp16(v) (RNE),
+//   lo = fp16(v - hi) (v - hi is exact in fp32, Sterbenz);
+// BF = true (gemm mode 2, bf16): blocks [NC][KB32][1 KiB] of bf16(v) (RNE).
 template <bool BF = false, class F>
 static float pack16(uint16_t* dst, int Kreal, int Nreal, int KB32, int NC, F w) {
+    constexpr size_t blk = BF ? 512 : 1024;      // uint16 per block
     float wmax = 0.f;
     for (int ct = 0; ct < NC; ++ct)
         for (int kb = 0; kb < KB32; ++kb)
             for (int lane = 0; lane < 64; ++lane)
                 for (int i = 0; i < 8; ++i) {
-                    const int k = kb * 32 + 8 * (lane >> 4) + i;
+                    const int g = lane >> 4;
+                    const int k = kb * 32 + (i < 4 ? 4 * g + i : 16 + 4 * g + (i - 4));
                     const int n = ct * 16 + (lane & 15);
                     const float v = (k < Kreal && n < Nreal) ? w(k, n) * W16_SCALE : 0.f;
                     wmax = fmaxf(wmax, fabsf(v));
-                    uint16_t hb, lb;
+                    const size_t base = (size_t)(ct * KB32 + kb) * blk;
                     if constexpr (BF) {
-                        hb = bf16_rne(v);
-                        lb = bf16_rne(v - bf16_to_f32(hb));
+                        dst[base + lane * 8 + i] = bf16_rne(v);
                     } else {
                         const _Float16 hi = (_Float16)v;
                         const _Float16 lo = (_Float16)(v - (float)hi);
-                        hb = __builtin_bit_cast(uint16_t, hi);
-                        lb = __builtin_bit_cast(uint16_t, lo);
+                        dst[base + lane * 8 + i] = __builtin_bit_cast(uint16_t, hi);
+                        dst[base + 512 + lane * 8 + i] = __builtin_bit_cast(uint16_t, lo);
                     }
-                    const size_t base = ((size_t)(ct * KB32 + kb) * BLK16) / 2;
-                    dst[base + lane * 8 + i] = hb;
-                    dst[base + 512 + lane * 8 + i] = lb;
                 }
     return wmax;
 }
 
-// Row of a ChebConv weight (3,1,96,out) viewed as [3*96][out] that multiplies column k of
-// cheb_prep's [T1X | T2X | X] buffer.
-static inline int cheb_row(int k) { return ((k / D + 1) % 3) * D + k % D; }
 
 // Chebyshev terms of the normalised Laplacian, fp32 in the reference's operation order
 // (ChebConv.py:114-130, :90-112): d = rowsum^-1/2; L = I - (d_i g_ij) d_j; T2 = 2 L@L - I.
@@ -577,8 +576,8 @@ static int upload(dpk_handle* h) {
     if (!h->arena) HIPCHK(h, hipMalloc(&h->arena, (size_t)ARENA_FLOATS * 4));
     if (!h->arena16) HIPCHK(h, hipMalloc(&h->arena16, (size_t)ARENA16_BYTES));
     HIPCHK(h, hipMemcpy(h->arena16, h->h_arena16.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
-    if (!h->arenabf) HIPCHK(h, hipMalloc(&h->arenabf, (size_t)ARENA16_BYTES));
-    HIPCHK(h, hipMemcpy(h->arenabf, h->h_arenabf.data(), (size_t)ARENA16_BYTES, hipMemcpyHostToDevice));
+    if (!h->arenabf) HIPCHK(h, hipMalloc(&h->arenabf, (size_t)ARENAB_BYTES));
+    HIPCHK(h, hipMemcpy(h->arenabf, h->h_arenabf.data(), (size_t)ARENAB_BYTES, hipMemcpyHostToDevice));
     if (!h->temb) HIPCHK(h, hipMalloc(&h->temb, (size_t)TEMB_FLOATS * 4));
     HIPCHK(h, hipMemcpy(h->arena, h->h_arena.data(), (size_t)ARENA_FLOATS * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(h->temb, h->h_temb.data(), (size_t)TEMB_FLOATS * 4, hipMemcpyHostToDevice));
@@ -803,7 +802,7 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     }
     h->h_arena.assign(ARENA_FLOATS, 0.f);
     h->h_arena16.assign(ARENA16_BYTES / 2, 0);
-    h->h_arenabf.assign(ARENA16_BYTES / 2, 0);
+    h->h_arenabf.assign(ARENAB_BYTES / 2, 0);
     h->h_temb.assign(TEMB_FLOATS, 0.f);
     *out = h;
     return DPK_OK;
@@ -1003,31 +1002,32 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         pack_blocks(Lw + OFF_O, D, D, KB_D, 6, [&](int k, int n) { return wo[n * D + k]; });
         pack_blocks(Lw + OFF_FC1, D, D2, KB_D, 12, [&](int k, int n) { return f1w[n * D + k]; });
         pack_blocks(Lw + OFF_FC2, D2, D, KB_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; });
-        // ChebConv weight (3,1,in,out): the fp32 GEMMs read [x | T1x | T2x] (x from its own buffer,
-        // cheb_prep XSKIP), the reference's row order; the split GEMMs read cheb_prep's one-buffer
-        // [T1x | T2x | x] (cheb_row)
+        // ChebConv weight (3,1,in,out): the GEMMs read [x | T1x | T2x] (x from its own buffer,
+        // cheb_prep XSKIP), the reference's row order
         pack_blocks(Lw + OFF_C1, D3, D, KB_D3, 6, [&](int k, int n) { return c1w[k * D + n]; });
         pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[k * D + n]; });
+        // the half-width-operand GEMMs (modes 1, 2) read the fp32 mode's operands: LN0 folded into QKV
+        // (bias OFF_CQKV), the Chebyshev GEMMs' [x | T1x | T2x] in the reference's row order
+        auto wqkv_f = [&](int k, int n) { return fold0 ? n0a[k] * wqkv(k, n) : wqkv(k, n); };
+        auto wo_f = [&](int k, int n) { return wo[n * D + k]; };
+        auto f1_f = [&](int k, int n) { return f1w[n * D + k]; };
+        auto f2_f = [&](int k, int n) { return f2w[n * D2 + k]; };
+        auto c1_f = [&](int k, int n) { return c1w[k * D + n]; };
+        auto c2_f = [&](int k, int n) { return c2w[k * D + n]; };
         uint16_t* L16 = h->h_arena16.data() + (size_t)l * LAYER16_BYTES / 2;
-        w16max = fmaxf(w16max, pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
-            const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
-            return w[(n % D) * D + k];
-        }));
-        w16max = fmaxf(w16max, pack16(L16 + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; }));
-        w16max = fmaxf(w16max, pack16(L16 + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; }));
-        w16max = fmaxf(w16max, pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; }));
-        w16max = fmaxf(w16max, pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; }));
-        w16max = fmaxf(w16max, pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; }));
-        uint16_t* Lb = h->h_arenabf.data() + (size_t)l * LAYER16_BYTES / 2;
-        (void)(pack16<true>(Lb + O16_QKV / 2, D, D3, KB32_D, 18, [&](int k, int n) {
-            const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
-            return w[(n % D) * D + k];
-        }));
-        (void)(pack16<true>(Lb + O16_O / 2, D, D, KB32_D, 6, [&](int k, int n) { return wo[n * D + k]; }));
-        (void)(pack16<true>(Lb + O16_FC1 / 2, D, D2, KB32_D, 12, [&](int k, int n) { return f1w[n * D + k]; }));
-        (void)(pack16<true>(Lb + O16_FC2 / 2, D2, D, KB32_D2, 6, [&](int k, int n) { return f2w[n * D2 + k]; }));
-        (void)(pack16<true>(Lb + O16_C1 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c1w[cheb_row(k) * D + n]; }));
-        (void)(pack16<true>(Lb + O16_C2 / 2, D3, D, KB32_D3, 6, [&](int k, int n) { return c2w[cheb_row(k) * D + n]; }));
+        w16max = fmaxf(w16max, pack16(L16 + O16_QKV / 2, D, D3, KB32_D, 18, wqkv_f));
+        w16max = fmaxf(w16max, pack16(L16 + O16_O / 2, D, D, KB32_D, 6, wo_f));
+        w16max = fmaxf(w16max, pack16(L16 + O16_FC1 / 2, D, D2, KB32_D, 12, f1_f));
+        w16max = fmaxf(w16max, pack16(L16 + O16_FC2 / 2, D2, D, KB32_D2, 6, f2_f));
+        w16max = fmaxf(w16max, pack16(L16 + O16_C1 / 2, D3, D, KB32_D3, 6, c1_f));
+        w16max = fmaxf(w16max, pack16(L16 + O16_C2 / 2, D3, D, KB32_D3, 6, c2_f));
+        uint16_t* Lb = h->h_arenabf.data() + (size_t)l * LAYER16_BYTES / 4;     // bf16 blocks: half the bytes
+        (void)pack16<true>(Lb + O16_QKV / 4, D, D3, KB32_D, 18, wqkv_f);
+        (void)pack16<true>(Lb + O16_O / 4, D, D, KB32_D, 6, wo_f);
+        (void)pack16<true>(Lb + O16_FC1 / 4, D, D2, KB32_D, 12, f1_f);
+        (void)pack16<true>(Lb + O16_FC2 / 4, D2, D, KB32_D2, 6, f2_f);
+        (void)pack16<true>(Lb + O16_C1 / 4, D3, D, KB32_D3, 6, c1_f);
+        (void)pack16<true>(Lb + O16_C2 / 4, D3, D, KB32_D3, 6, c2_f);
         for (int c = 0; c < D; ++c) {
             Lw[OFF_BQKV + c] = bq[c];
             Lw[OFF_BQKV + D + c] = bk[c];

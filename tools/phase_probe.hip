@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(NT, 1) probe(const float* W, float* out, long 
     for (int it = 0; it < iters; ++it) {
         if constexpr (PH == PH_LN) layer_norm(XS, B1, LNP, LNP + D, tid);
         else if constexpr (PH == PH_ATTN) attention_mma(B2, B1, 0x1ffffu, wave, lane);
-        else if constexpr (PH == PH_CHEB) cheb_prep<true, 0, true>(W + 1024, XS, B2, wave, lane);
+        else if constexpr (PH == PH_CHEB) cheb_prep<true, true>(W + 1024, XS, B2, wave, lane);
         else if constexpr (PH == PH_GRAPH1) graph_mma<false>(gf, B1, B1, nullptr, wave, lane);
         else if constexpr (PH == PH_GRAPH2) graph_mma<true>(gf, B1, XS, W + 2048, wave, lane);
         __syncthreads();

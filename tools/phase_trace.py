@@ -21,16 +21,19 @@ SO = os.environ.get("DPK_TRACE_SO", os.path.join(ROOT, "build", "trace", "libdpk
 
 # stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
 # ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
-# the split-fp16 GEMMs (gemm mode f16x3) run a wave's column tiles in passes of 3 and stamp per pass
+# the f16x3 GEMMs run a wave's column tiles in passes and stamp per pass
 def _events(gemm_mode="fp32", fused=None):
     # fp32 mode built with -DDPK_LN_FUSE=1: no LayerNorm phases (LN0 in the QKV operand, LN1 in graph1)
     if fused is None:
         fused = gemm_mode == "fp32" and os.environ.get("DPK_LN_FUSE", "0") == "1"
-    # fp32 mode with LN1 mapped wave = pose (DPK_LN1_POSE, the default): no barrier between LN1 and graph1
-    ln1pose = gemm_mode == "fp32" and not fused and os.environ.get("DPK_LN1_POSE", "1") == "1"
+    # LN1 mapped wave = pose (DPK_LN1_POSE, the default; every GEMM mode since round 5): no barrier
+    # between LN1 and graph1
+    ln1pose = not fused and os.environ.get("DPK_LN1_POSE", "1") == "1"
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
-    npass = {"QKV": 3, "fc1": 2} if gemm_mode in ("f16x3", "bf16") else {}
+    # the half-width-operand GEMMs run a wave's column tiles in passes (gemmh_wg): f16x3 QKV 3 x 3 tiles,
+    # fc1 2 x 3; bf16 one pass each
+    npass = {"QKV": 3, "fc1": 2} if gemm_mode == "f16x3" else {}
 
     def gemm(n):
         for _ in range(npass.get(n.split(".")[-1], 1)):
