@@ -43,8 +43,8 @@
 // buffer (end of k-loop, end of epilogue); empty in the library
 #if DPK_TRACE
 namespace dpk {
-__shared__ unsigned long long* tr_row[4];   // per-wave stamp row of the traced step (null: off)
-__shared__ int tr_ix[4];
+__shared__ unsigned long long* tr_row[8];   // per-wave stamp row of the traced step (null: off)
+__shared__ int tr_ix[8];
 __device__ __forceinline__ void tr_stamp() {
     const int w = threadIdx.x >> 6;
     if (tr_row[w] && (threadIdx.x & 63) == 0 && tr_ix[w] < 256) tr_row[w][tr_ix[w]] = __builtin_amdgcn_s_memtime();
@@ -127,52 +127,50 @@ namespace dpk {
 namespace dpk2 {
 #include "dpk_sampler.inc"
 }  // namespace dpk2
+// The persistent sampler at a wider model (round 5): hid 128 / 8 heads (d_k 16), 2-pose tiles (4-pose
+// tiles of 128-wide rows do not fit 160 KB of LDS), fp32 GEMMs; run by the generic-shape path for that
+// shape instead of its per-op launches (dpk_generic.inc, GenFused)
+#define DPK_P 2
+#undef DPK_D
+#undef DPK_NH
+#define DPK_D 128
+#define DPK_NH 8
+namespace dpkw {
+#include "dpk_sampler.inc"
+}  // namespace dpkw
+#undef DPK_NH
+#undef DPK_D
 #undef DPK_P
+// Measured-slower tile variants for the half-width-operand GEMM modes, built only
+// with -DDPK_EXPT_TILES=1 (tools/build_variant.sh) and selected at handle creation by DPK_CORES=1 / DPK_W8=1:
+//  * 2-pose tiles built for two workgroups per CU (the half-width MFMAs leave the SIMD free for the other
+//    workgroup's VALU work): bf16 config 3 107.3k vs 115.3k poses/s, f16x3 116k vs 153k (49 VGPRs spilled);
+//  * 4-pose tiles on 8 waves, two per SIMD: 223 VGPRs spilled under the 256-register budget, 2.1x slower.
+#ifndef DPK_EXPT_TILES
+#define DPK_EXPT_TILES 0
+#endif
+#if DPK_EXPT_TILES
+#undef DPK_WGCU
+#define DPK_WGCU 2
+namespace dpk2c {
+#include "dpk_sampler.inc"
+}  // namespace dpk2c
+#undef DPK_WGCU
+#undef DPK_P
+// 4-pose tiles on 8 waves, two per SIMD (gemm modes 1, 2: launch_tiles, DPK_W8)
+#define DPK_P 4
+#undef DPK_NW
+#define DPK_NW 8
+namespace dpk8 {
+#include "dpk_sampler.inc"
+}  // namespace dpk8
+#undef DPK_NW
+#undef DPK_P
+#endif  // DPK_EXPT_TILES
 
 namespace dpk {
 
 // ---------------------------------------------------------------------------------------
-// Timestep MLP (gcndiff.py:15-33, :103-106) and per-layer temb_proj(swish(.)) (:46, :51):
-// tproj[slot][l][:] for slot t-values (one per DDIM step, or one per pose in eps mode).
-// Batch-invariant in the sampler: all rows of a step share t, so it is computed once per step.
-__device__ __forceinline__ float swishf(float x) { return x * (1.0f / (1.0f + expf(-x))); }
-
-__global__ void __launch_bounds__(256) temb_kernel(const float* __restrict__ tw, const float* __restrict__ tvals,
-                                                   int tstride, float* __restrict__ tproj) {
-    __shared__ float emb[D];
-    __shared__ float h0[E];
-    __shared__ float h1[E];
-    const int tid = threadIdx.x;
-    const float t = tvals[(size_t)blockIdx.x * tstride];
-    const float neg_scale = -(float)(9.210340371976184 / 47.0);   // -(log(10000)/(half-1)), fp32 scalar
-    if (tid < D) {
-        const int k = tid < D / 2 ? tid : tid - D / 2;
-        const float f = expf((float)k * neg_scale);
-        const float arg = t * f;
-        emb[tid] = tid < D / 2 ? sinf(arg) : cosf(arg);
-    }
-    __syncthreads();
-    for (int o = tid; o < E; o += 256) {
-        float acc = 0.f;
-        for (int k = 0; k < D; ++k) acc = fmaf(emb[k], tw[TOFF_W0 + k * E + o], acc);
-        h0[o] = swishf(acc + tw[TOFF_B0 + o]);
-    }
-    __syncthreads();
-    for (int o = tid; o < E; o += 256) {
-        float acc = 0.f;
-        for (int k = 0; k < E; ++k) acc = fmaf(h0[k], tw[TOFF_W1 + k * E + o], acc);
-        h1[o] = swishf(acc + tw[TOFF_B1 + o]);     // swish(temb) as consumed by every temb_proj
-    }
-    __syncthreads();
-    for (int o = tid; o < NL * D; o += 256) {
-        const int l = o / D, c = o - l * D;
-        const float* wp = tw + TOFF_WP + (size_t)l * E * D;
-        float acc = 0.f;
-        for (int k = 0; k < E; ++k) acc = fmaf(h1[k], wp[k * D + c], acc);
-        tproj[(size_t)blockIdx.x * NL * D + o] = acc + tw[TOFF_BP + o];
-    }
-}
-
 // Elementwise DDIM update for externally computed eps; z from the caller's draws of this step
 // (`noise`, n floats) or counter-based.
 __global__ void __launch_bounds__(256) ddim_kernel(const float* __restrict__ xt, const float* __restrict__ et,
@@ -269,6 +267,8 @@ struct dpk_handle {
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int n_cu = 256;                // compute units of the device (workgroups per round)
     int tail_plan = 2;             // dpk_set_tail_plan: 0 4-pose tiles, 1 2-pose tail round, 2 step split
+    bool coresident = false;       // gemm modes 1, 2: 2-pose tiles, two workgroups per CU (DPK_CORES=1)
+    bool w8 = false;               // gemm modes 1, 2: 4-pose tiles on 8 waves (DPK_W8=1)
     unsigned* flags = nullptr;     // device: FLAG_SLOTS x n_cu step-split handoff words (zero between launches),
                                    // then the split fallback counter
     std::vector<int> slot_free;    // flag slots no launch holds
@@ -673,8 +673,30 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
         if (h->sparse_graph) DPK_LAUNCH3(NS, true, 0);                                                          \
         else DPK_LAUNCH3(NS, false, 0);                                                                         \
     } while (0)
-    if constexpr (PT == 4) DPK_LAUNCH(dpk);
-    else DPK_LAUNCH(dpk2);
+    if constexpr (PT == 4) {
+        if (DPK_EXPT_TILES && h->w8 && gm != 0) {
+#if DPK_EXPT_TILES
+            // 8-wave 4-pose tiles: only the half-width-operand GEMM modes are instantiated
+            const dim3 block8(dpk8::NT);
+#define DPK_LAUNCH8(SP, NZ)                                                                                          \
+    do {                                                                                                           \
+        if (gm == 1) hipLaunchKernelGGL((dpk8::sample_kernel<MODE, SP, 1, NZ>), grid, block8, shmem, st, a, h->arena, a16); \
+        else hipLaunchKernelGGL((dpk8::sample_kernel<MODE, SP, 2, NZ>), grid, block8, shmem, st, a, h->arena, a16);       \
+    } while (0)
+            const int nz = (MODE == M_SAMPLE && a.noise) ? 1 : (MODE == M_SAMPLE && !DPK_ZM0_PHILOX && a.eta != 0.f) ? 2 : 0;
+            if (h->sparse_graph) {
+                if (nz == 1) DPK_LAUNCH8(true, 1); else if (nz == 2) DPK_LAUNCH8(true, 2); else DPK_LAUNCH8(true, 0);
+            } else {
+                if (nz == 1) DPK_LAUNCH8(false, 1); else if (nz == 2) DPK_LAUNCH8(false, 2); else DPK_LAUNCH8(false, 0);
+            }
+#undef DPK_LAUNCH8
+            return;
+#endif
+        }
+        DPK_LAUNCH(dpk);
+    } else {
+        DPK_LAUNCH(dpk2);
+    }
 #undef DPK_LAUNCH
 #undef DPK_LAUNCH3
 }
@@ -696,6 +718,28 @@ template <int MODE>
 static int launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap) {
     const int N = a.N;
     const int round4 = P * h->n_cu;
+    if constexpr (MODE == M_SAMPLE) {
+        // co-resident 2-pose tiles, two workgroups per CU (gemm modes 1, 2; DPK_CORES=1)
+        if (DPK_EXPT_TILES && h->coresident && h->gemm_mode != 0) {
+#if DPK_EXPT_TILES
+            a.pose_off = 0;
+            const dim3 grid((N + 1) / 2), block(NT);
+            const char* a16 = h->gemm_mode == 2 ? h->arenabf : h->arena16;
+#define DPK_LAUNCH_C(SP, G, NZ) hipLaunchKernelGGL((dpk2c::sample_kernel<MODE, SP, G, NZ>), grid, block, 0, st, a, h->arena, a16)
+            const int nz = a.noise ? 1 : (!DPK_ZM0_PHILOX && a.eta != 0.f) ? 2 : 0;
+            if (h->sparse_graph) {
+                if (h->gemm_mode == 1) { if (nz == 1) DPK_LAUNCH_C(true, 1, 1); else if (nz == 2) DPK_LAUNCH_C(true, 1, 2); else DPK_LAUNCH_C(true, 1, 0); }
+                else { if (nz == 1) DPK_LAUNCH_C(true, 2, 1); else if (nz == 2) DPK_LAUNCH_C(true, 2, 2); else DPK_LAUNCH_C(true, 2, 0); }
+            } else {
+                if (h->gemm_mode == 1) { if (nz == 1) DPK_LAUNCH_C(false, 1, 1); else if (nz == 2) DPK_LAUNCH_C(false, 1, 2); else DPK_LAUNCH_C(false, 1, 0); }
+                else { if (nz == 1) DPK_LAUNCH_C(false, 2, 1); else if (nz == 2) DPK_LAUNCH_C(false, 2, 2); else DPK_LAUNCH_C(false, 2, 0); }
+            }
+#undef DPK_LAUNCH_C
+            HIPCHK(h, hipGetLastError());
+            return DPK_OK;
+#endif
+        }
+    }
     if constexpr (MODE == M_SAMPLE) {
         const int tiles = (N + P - 1) / P, q = tiles / h->n_cu, r = tiles % h->n_cu;
         if (h->tail_plan == 2 && a.K >= 2 && q >= 1 && r > 0 && 2 * r <= h->n_cu) {
@@ -789,6 +833,8 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     h->n_cu = std::max(h->n_cu, 1);
     // DPK_TAIL_SPLIT=0/1/2: the initial tail plan (A/B timing); trace builds stamp per block id
     if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_plan = std::min(std::max(atoi(ts), 0), 2);
+    if (const char* cr = getenv("DPK_CORES")) h->coresident = atoi(cr) != 0;
+    if (const char* w8 = getenv("DPK_W8")) h->w8 = atoi(w8) != 0 && !DPK_TRACE;
     if (DPK_TRACE) h->tail_plan = 0;
     // FLAG_SLOTS x n_cu handoff words + the fallback counter
     const size_t flag_bytes = ((size_t)FLAG_SLOTS * h->n_cu + 4) * 4;

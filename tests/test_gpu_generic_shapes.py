@@ -313,3 +313,70 @@ def test_generic_eta_with_caller_noise_vs_oracle(dev):
     rxs, _ = O.generalized_steps(x, ones, seq, fwd, _betas(), eta=0.6, noise=z)
     assert record_delta(_maxdiff(xs, torch.stack(rxs)), TOL)
     m.close()
+
+
+def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch):
+    """hid 128 / 8 heads / 17 joints runs the persistent sampler compiled at that width (dpkw, 2-pose
+    tiles, round 5) instead of the per-op launches: eps (handle-wide and per-pose masks), the K=10
+    trajectory, eta > 0 with the caller's draws, a dense (non-H36M) adjacency and 1..5 layers agree with
+    the per-op path (DPK_GEN_FUSED=0) and the oracle within the fp32 bars."""
+    from oracle import gcndiff_oracle as O
+
+    x = _inputs(37, 17, seed=91)
+    t = torch.arange(37, dtype=torch.float32) * 1.5
+    ones = torch.ones(1, 1, 17, dtype=torch.bool)
+    per = torch.ones(37, 1, 17, dtype=torch.bool)
+    per[::3, 0, 2::3] = False
+    seq = make_seq("uniform", 50, 10)
+    z = torch.randn((10,) + tuple(x.shape), generator=torch.Generator().manual_seed(5))
+    rng = np.random.default_rng(3)
+    dense = adj_mx_from_edges() + 0.1 * (rng.random((17, 17)) > 0.6)
+    dense = ((dense + dense.T) / 2).astype(np.float32)
+    for layers, adj in ((5, adj_mx_from_edges()), (2, dense)):
+        sd = synthetic_state_dict(hid=128, n_layers=layers)
+        res = {}
+        for fused in ("1", "0"):
+            monkeypatch.setenv("DPK_GEN_FUSED", fused)
+            m = HipGCNdiff(adj, _cfg(128, 8, layers, 17), device=dev)
+            m.load_state_dict(sd)
+            res[fused] = (m(x.to(dev), ones.to(dev), t.to(dev), 0), m(x.to(dev), per.to(dev), t.to(dev), 0),
+                          m.sample(x.to(dev), seq, _betas(), mask=ones.to(dev), trajectory=True)[0],
+                          m.sample(x.to(dev), seq, _betas(), eta=0.7, mask=ones.to(dev), noise=z.to(dev)))
+            m.close()
+        for a, b in zip(res["1"], res["0"]):
+            assert record_delta(_maxdiff(a, b), TOL)
+        P = O.params_to_torch(sd)
+        fwd = lambda a, mk, tt: O.gcndiff_forward(P, torch.from_numpy(adj), a, mk, tt, n_layers=layers, heads=8)  # noqa: E731
+        assert record_delta(_maxdiff(res["1"][0], fwd(x, ones, t)), TOL)
+        assert record_delta(_maxdiff(res["1"][1], fwd(x, per, t)), TOL)
+        rxs, _ = O.generalized_steps(x, ones, seq, fwd, _betas())
+        assert record_delta(_maxdiff(res["1"][2], torch.stack(rxs)), TOL)
+        rz, _ = O.generalized_steps(x, ones, seq, fwd, _betas(), eta=0.7, noise=z)
+        assert record_delta(_maxdiff(res["1"][3], rz[-1]), TOL)
+
+
+def test_fused_wide_sampler_under_capture(dev):
+    """The fused wide-model sampler inside a caller's torch.cuda.graph (its per-call timestep
+    projections in the capture's scratch): replays bitwise equal to eager."""
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(128, 8, 2, 17), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=128, n_layers=2))
+    ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
+    x = _inputs(30, 17, seed=92).to(dev)
+    seq = make_seq("uniform", 50, 5)
+    eager = m.sample(x, seq, _betas(), mask=ones).clone()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        m.sample(x, seq, _betas(), mask=ones)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    out = torch.empty_like(x)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.sample(x, seq, _betas(), mask=ones, out=out)
+    for _ in range(2):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(out, eager)
+    del g
+    m.close()

@@ -17,15 +17,18 @@ from diffpose_amd.schedule import get_beta_schedule, make_seq  # noqa: E402
 from diffpose_amd.weights import synthetic_state_dict  # noqa: E402
 
 
-def run(label, hid, heads, layers, force=False, n=1024, k=50):
+def run(label, hid, heads, layers, force=False, n=1024, k=50, per_op=False):
     cfg = ns(model=ns(hid_dim=hid, emd_dim=hid, coords_dim=[5, 5], num_layer=layers, n_head=heads, dropout=0.0,
                       n_pts=17))
     if force:
         os.environ["DPK_FORCE_GENERIC"] = "1"
+    if per_op:                     # the per-op launches even where a fused width instance exists
+        os.environ["DPK_GEN_FUSED"] = "0"
     try:
         m = HipGCNdiff(adj_mx_from_edges(), cfg, device="cuda:0")
     finally:
         os.environ.pop("DPK_FORCE_GENERIC", None)
+        os.environ.pop("DPK_GEN_FUSED", None)
     m.load_state_dict(synthetic_state_dict(hid=hid, n_layers=layers))
     x = torch.from_numpy(synthetic_batch(n, seed=1)[0]).cuda()
     seq = make_seq("uniform", 50, k)
@@ -51,4 +54,5 @@ if __name__ == "__main__":
     run("persistent sampler, hid 96 / 4 heads / 5 layers", 96, 4, 5)
     run("generic path (forced), hid 96 / 4 heads / 5 layers", 96, 4, 5, force=True)
     run("generic path, hid 64 / 2 heads / 2 layers", 64, 2, 2)
-    run("generic path, hid 128 / 8 heads / 5 layers", 128, 8, 5)
+    run("generic path per-op, hid 128 / 8 heads / 5 layers", 128, 8, 5, per_op=True)
+    run("fused wide sampler (dpkw), hid 128 / 8 heads / 5 layers", 128, 8, 5)
