@@ -501,14 +501,16 @@ static bool drain_relaxed() {
     return se == hipSuccess;
 }
 
-// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  The release
-// callback may run while a replay is still in flight on some stream, so the device is drained once
-// before anything is reused (graph destruction is rare; nothing waits otherwise).
+// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  No drain: the release
+// callback runs when the graph's executable is destroyed, and on this runtime destroying an executable
+// waits for its launches in flight (tools/probe_user_object_release.py: deleting a CUDAGraph 0.1 ms after
+// its 175 ms replay was enqueued returned when the replay had finished, and `released` was never seen
+// set while it ran), so nothing the capture reads is still in use.  (Round 4 drained the device here;
+// from another thread during a global-mode capture that invalidated the capture, advisor r04.)
 static void cap_sweep(dpk_handle* h) {
     bool any = false;
     for (CapRes* c : h->caps) any = any || (c->tracked && c->released.load());
     if (!any) return;
-    if (!drain_relaxed()) return;     // a stream of the device is capturing: the resources wait for a later call
     std::vector<CapRes*> keep;
     for (CapRes* c : h->caps) {
         if (!(c->tracked && c->released.load())) {

@@ -22,7 +22,7 @@ os.environ["DPK_CAPTURE_RELEASE"] = "1"
 dev = torch.device("cuda", 0)
 m = HipGCNdiff(adj_mx_from_edges(), None, device=dev)
 m.load_state_dict(synthetic_state_dict())
-x = torch.from_numpy(synthetic_batch(4096, seed=1)[0]).to(dev)
+x = torch.from_numpy(synthetic_batch(8192, seed=1)[0]).to(dev)
 b = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3, num_diffusion_timesteps=101)).float()
 seq = make_seq("uniform", 100, 100)
 out = torch.empty_like(x)
@@ -41,8 +41,16 @@ for trial in range(3):
     t0 = time.perf_counter()
     g.replay()
     done.record()
+    t_rep = (time.perf_counter() - t0) * 1e3
+    pending0 = not done.query()
     del g
+    t_del = (time.perf_counter() - t0) * 1e3
     gc.collect()
+    t_gc = (time.perf_counter() - t0) * 1e3
+    pending1 = not done.query()
+    rel1 = m.debug_resources()["released"]
+    print(f"  replay enqueued at {t_rep:.1f} ms (pending {pending0}); graph deleted at {t_del:.1f} ms, gc done at "
+          f"{t_gc:.1f} ms: replay still pending {pending1}, released {rel1}")
     seen = []
     while not done.query():
         seen.append((round((time.perf_counter() - t0) * 1e3, 2), m.debug_resources()["released"]))
