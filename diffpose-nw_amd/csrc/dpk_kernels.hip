@@ -130,6 +130,7 @@ namespace dpk2 {
 // The persistent sampler at a wider model (round 5): hid 128 / 8 heads (d_k 16), 2-pose tiles (4-pose
 // tiles of 128-wide rows do not fit 160 KB of LDS), fp32 GEMMs; run by the generic-shape path for that
 // shape instead of its per-op launches (dpk_generic.inc, GenFused)
+#undef DPK_P
 #define DPK_P 2
 #undef DPK_D
 #undef DPK_NH
@@ -150,6 +151,7 @@ namespace dpkw {
 #define DPK_EXPT_TILES 0
 #endif
 #if DPK_EXPT_TILES
+#define DPK_P 2
 #undef DPK_WGCU
 #define DPK_WGCU 2
 namespace dpk2c {
