@@ -556,7 +556,7 @@ def rank_main(args):
                      "tolerance_mm": 1e-4, "pass": abs(m_h - m_r) <= 1e-4}
                 if gemm == "bf16":   # reduced precision: the delta IS the tolerance-study result
                     r.update({"tolerance_mm": None, "pass": None,
-                              "note": "tolerance study (BASELINE config 3): bf16 GEMM operands; the fp32 bar is 1e-4 mm"})
+                              "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs and of attention's score and P.V products; the fp32 bar is 1e-4 mm"})
                 return r
             result["parity"] = parity(out_main, args.gemm)
             for g, v in variants.items():

@@ -142,6 +142,16 @@ namespace dpkw {
 #undef DPK_NH
 #undef DPK_D
 #undef DPK_P
+// ... and at hid 64 / 2 heads (d_k 32), 4-pose tiles (117 KB of LDS), the generic-shape test model's width
+#define DPK_P 4
+#define DPK_D 64
+#define DPK_NH 2
+namespace dpkn {
+#include "dpk_sampler.inc"
+}  // namespace dpkn
+#undef DPK_NH
+#undef DPK_D
+#undef DPK_P
 // Measured-slower tile variants for the half-width-operand GEMM modes, built only
 // with -DDPK_EXPT_TILES=1 (tools/build_variant.sh) and selected at handle creation by DPK_CORES=1 / DPK_W8=1:
 //  * 2-pose tiles built for two workgroups per CU (the half-width MFMAs leave the SIMD free for the other

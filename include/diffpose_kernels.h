@@ -82,9 +82,12 @@ int dpk_version(void);
  * (models/gcndiff.py:55-99; runners/diffpose_frame.py:118-127).  The shape every reference config
  * uses (hid_dim 96, n_head 4, n_pts 17, num_layer 1..5, coords [5,5] or GCNpose's [2,3]) runs the
  * persistent sampler; any other shape with hid_dim a multiple of n_head, n_pts <= 32 and coords
- * in == out (or [2,3]) runs the generic-shape path: the same model as per-op HIP kernels, fp32 GEMMs
- * only (dpk_set_gemm_mode 1/2 then fail with DPK_E_UNSUPPORTED), no graph capture (a captured call
- * fails with DPK_E_UNSUPPORTED), per-stream scratch grown on demand.  Other shapes:
+ * in == out (or [2,3]) runs the generic-shape path: the same model as per-op HIP kernels, or, for GCNdiff
+ * at hid_dim 128 / n_head 8 and hid_dim 64 / n_head 2 on 17 joints (num_layer <= 5, coords [5,5]), the
+ * persistent sampler compiled at that width (round 5); fp32 GEMMs only (dpk_set_gemm_mode 1/2 then fail
+ * with DPK_E_UNSUPPORTED), per-stream scratch grown on demand; under a caller's stream capture the
+ * launches are recorded into the caller's graph from a capture-owned scratch (round 5; the first capture
+ * of a size needs one uncaptured call of at least that size, else DPK_E_STATE).  Other shapes:
  * DPK_E_UNSUPPORTED. */
 int dpk_create(const dpk_config* cfg, dpk_handle** out);
 
@@ -220,8 +223,10 @@ int dpk_gmm_sample_f64(const double* gmm_dev, const double* poses3d_dev, int n_s
  *   mode 1: 3-term fp16 split (a = a_hi + a_lo, w*64 = w_hi + w_lo; a_hi w_hi + a_hi w_lo +
  *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products;
  *   mode 2: bf16 (a and w rounded to bf16, one v_mfma_f32_16x16x32_bf16 product, fp32
- *           accumulate): a reduced-precision mode for the tolerance study of BASELINE config 3.
- * The input/output ChebConvs, LayerNorm, attention and the DDIM update stay fp32 in all modes.
+ *           accumulate; since round 5 also attention's score and P.V products): a reduced-precision
+ *           mode for the tolerance study of BASELINE config 3.
+ * The input/output ChebConvs, LayerNorm, the softmax, the graph products and the DDIM update stay fp32
+ * in all modes, and so does attention in modes 0 and 1.
  * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle.  Range: mode 1 needs
  * every GEMM weight |w| < 1015 (else those calls return DPK_E_UNSUPPORTED) and GEMM inputs
  * (LayerNorm/attention/graph/Chebyshev outputs) below 65504 in magnitude; an overflow there

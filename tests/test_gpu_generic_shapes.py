@@ -65,10 +65,14 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("hid,heads,layers,npts,edges", SHAPES)
-def test_generic_eps_and_sample_vs_oracle(dev, hid, heads, layers, npts, edges):
+def test_generic_eps_and_sample_vs_oracle(dev, monkeypatch, hid, heads, layers, npts, edges, fused):
+    """fused "1": hid 128 / 8 heads and hid 64 / 2 heads on 17 joints run a persistent-sampler instance
+    (dpkw, dpkn; round 5), the 16-joint chain the per-op path; "0" (DPK_GEN_FUSED=0): all per-op."""
     from oracle import gcndiff_oracle as O
 
+    monkeypatch.setenv("DPK_GEN_FUSED", fused)
     sd = synthetic_state_dict(hid=hid, n_layers=layers, n_pts=npts)
     adj = adj_mx_from_edges(npts, edges)
     m = HipGCNdiff(adj, _cfg(hid, heads, layers, npts), device=dev)
@@ -147,12 +151,15 @@ def test_generic_gcnpose_vs_oracle(dev):
     m.close()
 
 
-def test_generic_path_under_caller_capture(dev):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_generic_path_under_caller_capture(dev, monkeypatch, fused):
     """A caller's torch.cuda.graph around the generic path (config 5's pattern, common/utils_diff.py:46-68
     called from runners/diffpose_frame.py:365): the launches are recorded into the caller's graph on the
     capture's own scratch (the model's spare, sized by the uncaptured warm-up), and every replay is
-    bitwise the eager result, for dpk_sample (K=4), dpk_eps, a captured loop of two samples on one
-    stream, and GCNpose; the scratch returns to the spare when the graph is destroyed."""
+    bitwise the eager result, for dpk_sample (K=4), dpk_eps and a captured loop of two samples on one
+    stream; the scratch returns to the spare when the graph is destroyed.  fused "0": the per-op
+    launches (DPK_GEN_FUSED=0); "1": the hid-64 persistent-sampler instance (dpkn)."""
+    monkeypatch.setenv("DPK_GEN_FUSED", fused)
     hid, heads, layers = 64, 2, 2
     m = HipGCNdiff(adj_mx_from_edges(), _cfg(hid, heads, layers, 17), device=dev)
     m.load_state_dict(synthetic_state_dict(hid=hid, n_layers=layers))
@@ -196,7 +203,9 @@ def test_generic_path_under_caller_capture(dev):
     m.close()
 
 
-def test_generic_capture_without_warmup_is_refused(dev):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_generic_capture_without_warmup_is_refused(dev, monkeypatch, fused):
+    monkeypatch.setenv("DPK_GEN_FUSED", fused)
     m = HipGCNdiff(adj_mx_from_edges(), _cfg(64, 2, 1, 17), device=dev)
     m.load_state_dict(synthetic_state_dict(hid=64, n_layers=1))
     x = _inputs(8, 17, seed=70).to(dev)
@@ -209,10 +218,11 @@ def test_generic_capture_without_warmup_is_refused(dev):
     m.close()
 
 
-def test_generic_eta0_seed_shares_one_loop_graph(dev):
+def test_generic_eta0_seed_shares_one_loop_graph(dev, monkeypatch):
     """advisor r04: at eta = 0 the seed is not read, so calls that differ only in seed (test_hyber
     passes seed + i per batch) replay one recorded loop instead of recording one each; at eta > 0
-    the seed keys the graph (the counter-based draws depend on it)."""
+    the seed keys the graph (the counter-based draws depend on it).  (Per-op path: DPK_GEN_FUSED=0.)"""
+    monkeypatch.setenv("DPK_GEN_FUSED", "0")
     m = HipGCNdiff(adj_mx_from_edges(), _cfg(64, 2, 1, 17), device=dev)
     m.load_state_dict(synthetic_state_dict(hid=64, n_layers=1))
     ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
@@ -268,7 +278,8 @@ def test_generic_loop_graph_matches_direct_launches(dev, monkeypatch):
     batch size, mask and seed) and replays it: bitwise the directly launched loop (DPK_GEN_GRAPH=0),
     across a new key after every change — a per-pose mask, another schedule, a larger batch (the
     scratch grows, the graphs over the old buffer are dropped), eta > 0 with another seed — and when
-    an earlier key comes back."""
+    an earlier key comes back.  (Per-op path: DPK_GEN_FUSED=0.)"""
+    monkeypatch.setenv("DPK_GEN_FUSED", "0")
     hid, heads, layers = 64, 2, 2
     sd = synthetic_state_dict(hid=hid, n_layers=layers)
     m = HipGCNdiff(adj_mx_from_edges(), _cfg(hid, heads, layers, 17), device=dev)
@@ -292,12 +303,14 @@ def test_generic_loop_graph_matches_direct_launches(dev, monkeypatch):
     m.close()
 
 
-def test_generic_eta_with_caller_noise_vs_oracle(dev):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_generic_eta_with_caller_noise_vs_oracle(dev, monkeypatch, fused):
     """eta > 0 on the generic path with the caller's draws (dpk_sample_noise; the launches go
     straight to the stream, the recorded loop only covers eta's counter-based draws): the K=10
     trajectory equals the oracle's run on the same draws within the bar."""
     from oracle import gcndiff_oracle as O
 
+    monkeypatch.setenv("DPK_GEN_FUSED", fused)
     hid, heads, layers = 64, 2, 2
     sd = synthetic_state_dict(hid=hid, n_layers=layers)
     adj = adj_mx_from_edges()
@@ -315,11 +328,13 @@ def test_generic_eta_with_caller_noise_vs_oracle(dev):
     m.close()
 
 
-def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch):
-    """hid 128 / 8 heads / 17 joints runs the persistent sampler compiled at that width (dpkw, 2-pose
-    tiles, round 5) instead of the per-op launches: eps (handle-wide and per-pose masks), the K=10
-    trajectory, eta > 0 with the caller's draws, a dense (non-H36M) adjacency and 1..5 layers agree with
-    the per-op path (DPK_GEN_FUSED=0) and the oracle within the fp32 bars."""
+@pytest.mark.parametrize("hid,heads", [(128, 8), (64, 2)])
+def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch, hid, heads):
+    """hid 128 / 8 heads and hid 64 / 2 heads on 17 joints run the persistent sampler compiled at that
+    width (dpkw: 2-pose tiles, d_k 16; dpkn: 4-pose tiles, d_k 32; round 5) instead of the per-op
+    launches: eps (handle-wide and per-pose masks), the K=10 trajectory, eta > 0 with the caller's
+    draws, a dense (non-H36M) adjacency and 2 and 5 layers agree with the per-op path (DPK_GEN_FUSED=0)
+    and the oracle within the fp32 bars."""
     from oracle import gcndiff_oracle as O
 
     x = _inputs(37, 17, seed=91)
@@ -333,11 +348,11 @@ def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch):
     dense = adj_mx_from_edges() + 0.1 * (rng.random((17, 17)) > 0.6)
     dense = ((dense + dense.T) / 2).astype(np.float32)
     for layers, adj in ((5, adj_mx_from_edges()), (2, dense)):
-        sd = synthetic_state_dict(hid=128, n_layers=layers)
+        sd = synthetic_state_dict(hid=hid, n_layers=layers)
         res = {}
         for fused in ("1", "0"):
             monkeypatch.setenv("DPK_GEN_FUSED", fused)
-            m = HipGCNdiff(adj, _cfg(128, 8, layers, 17), device=dev)
+            m = HipGCNdiff(adj, _cfg(hid, heads, layers, 17), device=dev)
             m.load_state_dict(sd)
             res[fused] = (m(x.to(dev), ones.to(dev), t.to(dev), 0), m(x.to(dev), per.to(dev), t.to(dev), 0),
                           m.sample(x.to(dev), seq, _betas(), mask=ones.to(dev), trajectory=True)[0],
@@ -346,7 +361,7 @@ def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch):
         for a, b in zip(res["1"], res["0"]):
             assert record_delta(_maxdiff(a, b), TOL)
         P = O.params_to_torch(sd)
-        fwd = lambda a, mk, tt: O.gcndiff_forward(P, torch.from_numpy(adj), a, mk, tt, n_layers=layers, heads=8)  # noqa: E731
+        fwd = lambda a, mk, tt: O.gcndiff_forward(P, torch.from_numpy(adj), a, mk, tt, n_layers=layers, heads=heads)  # noqa: E731
         assert record_delta(_maxdiff(res["1"][0], fwd(x, ones, t)), TOL)
         assert record_delta(_maxdiff(res["1"][1], fwd(x, per, t)), TOL)
         rxs, _ = O.generalized_steps(x, ones, seq, fwd, _betas())
@@ -355,11 +370,12 @@ def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch):
         assert record_delta(_maxdiff(res["1"][3], rz[-1]), TOL)
 
 
-def test_fused_wide_sampler_under_capture(dev):
-    """The fused wide-model sampler inside a caller's torch.cuda.graph (its per-call timestep
+@pytest.mark.parametrize("hid,heads", [(128, 8), (64, 2)])
+def test_fused_wide_sampler_under_capture(dev, hid, heads):
+    """The fused other-width samplers inside a caller's torch.cuda.graph (their per-call timestep
     projections in the capture's scratch): replays bitwise equal to eager."""
-    m = HipGCNdiff(adj_mx_from_edges(), _cfg(128, 8, 2, 17), device=dev)
-    m.load_state_dict(synthetic_state_dict(hid=128, n_layers=2))
+    m = HipGCNdiff(adj_mx_from_edges(), _cfg(hid, heads, 2, 17), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=hid, n_layers=2))
     ones = torch.ones(1, 1, 17, dtype=torch.bool, device=dev)
     x = _inputs(30, 17, seed=92).to(dev)
     seq = make_seq("uniform", 50, 5)

@@ -53,6 +53,9 @@ if __name__ == "__main__":
         sys.exit(0)
     run("persistent sampler, hid 96 / 4 heads / 5 layers", 96, 4, 5)
     run("generic path (forced), hid 96 / 4 heads / 5 layers", 96, 4, 5, force=True)
-    run("generic path, hid 64 / 2 heads / 2 layers", 64, 2, 2)
+    run("generic path per-op, hid 64 / 2 heads / 2 layers", 64, 2, 2, per_op=True)
+    run("fused sampler (dpkn), hid 64 / 2 heads / 2 layers", 64, 2, 2)
+    run("generic path per-op, hid 64 / 2 heads / 5 layers", 64, 2, 5, per_op=True)
+    run("fused sampler (dpkn), hid 64 / 2 heads / 5 layers", 64, 2, 5)
     run("generic path per-op, hid 128 / 8 heads / 5 layers", 128, 8, 5, per_op=True)
     run("fused wide sampler (dpkw), hid 128 / 8 heads / 5 layers", 128, 8, 5)
