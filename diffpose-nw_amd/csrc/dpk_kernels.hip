@@ -142,13 +142,29 @@ namespace dpkw {
 #undef DPK_NH
 #undef DPK_D
 #undef DPK_P
-// ... and at hid 64 / 2 heads (d_k 32), 4-pose tiles (117 KB of LDS), the generic-shape test model's width
+// ... at hid 128 / 4 heads (d_k 32), 2-pose tiles
+#define DPK_P 2
+#define DPK_D 128
+#define DPK_NH 4
+namespace dpkw4 {
+#include "dpk_sampler.inc"
+}  // namespace dpkw4
+#undef DPK_NH
+#undef DPK_D
+#undef DPK_P
+// ... and at hid 64 / 2 heads (d_k 32; the generic-shape tests' width) and hid 64 / 4 heads (d_k 16), 4-pose
+// tiles (129 KB of LDS)
 #define DPK_P 4
 #define DPK_D 64
 #define DPK_NH 2
 namespace dpkn {
 #include "dpk_sampler.inc"
 }  // namespace dpkn
+#undef DPK_NH
+#define DPK_NH 4
+namespace dpkn4 {
+#include "dpk_sampler.inc"
+}  // namespace dpkn4
 #undef DPK_NH
 #undef DPK_D
 #undef DPK_P

@@ -83,7 +83,7 @@ int dpk_version(void);
  * uses (hid_dim 96, n_head 4, n_pts 17, num_layer 1..5, coords [5,5] or GCNpose's [2,3]) runs the
  * persistent sampler; any other shape with hid_dim a multiple of n_head, n_pts <= 32 and coords
  * in == out (or [2,3]) runs the generic-shape path: the same model as per-op HIP kernels, or, for GCNdiff
- * at hid_dim 128 / n_head 8 and hid_dim 64 / n_head 2 on 17 joints (num_layer <= 5, coords [5,5]), the
+ * at hid_dim 128 / n_head 8 or 4 and hid_dim 64 / n_head 2 or 4 on 17 joints (num_layer <= 5, coords [5,5]), the
  * persistent sampler compiled at that width (round 5); fp32 GEMMs only (dpk_set_gemm_mode 1/2 then fail
  * with DPK_E_UNSUPPORTED), per-stream scratch grown on demand; under a caller's stream capture the
  * launches are recorded into the caller's graph from a capture-owned scratch (round 5; the first capture

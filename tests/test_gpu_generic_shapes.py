@@ -328,11 +328,11 @@ def test_generic_eta_with_caller_noise_vs_oracle(dev, monkeypatch, fused):
     m.close()
 
 
-@pytest.mark.parametrize("hid,heads", [(128, 8), (64, 2)])
+@pytest.mark.parametrize("hid,heads", [(128, 8), (128, 4), (64, 2), (64, 4)])
 def test_fused_wide_sampler_matches_per_op_path(dev, monkeypatch, hid, heads):
-    """hid 128 / 8 heads and hid 64 / 2 heads on 17 joints run the persistent sampler compiled at that
-    width (dpkw: 2-pose tiles, d_k 16; dpkn: 4-pose tiles, d_k 32; round 5) instead of the per-op
-    launches: eps (handle-wide and per-pose masks), the K=10 trajectory, eta > 0 with the caller's
+    """hid 128 / 8 or 4 heads and hid 64 / 2 or 4 heads on 17 joints run the persistent sampler compiled
+    at that width (dpkw, dpkw4: 2-pose tiles, d_k 16 / 32; dpkn, dpkn4: 4-pose tiles, d_k 32 / 16; round 5)
+    instead of the per-op launches: eps (handle-wide and per-pose masks), the K=10 trajectory, eta > 0 with the caller's
     draws, a dense (non-H36M) adjacency and 2 and 5 layers agree with the per-op path (DPK_GEN_FUSED=0)
     and the oracle within the fp32 bars."""
     from oracle import gcndiff_oracle as O

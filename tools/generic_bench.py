@@ -59,3 +59,7 @@ if __name__ == "__main__":
     run("fused sampler (dpkn), hid 64 / 2 heads / 5 layers", 64, 2, 5)
     run("generic path per-op, hid 128 / 8 heads / 5 layers", 128, 8, 5, per_op=True)
     run("fused wide sampler (dpkw), hid 128 / 8 heads / 5 layers", 128, 8, 5)
+    run("generic path per-op, hid 128 / 4 heads / 5 layers", 128, 4, 5, per_op=True)
+    run("fused sampler (dpkw4), hid 128 / 4 heads / 5 layers", 128, 4, 5)
+    run("generic path per-op, hid 64 / 4 heads / 5 layers", 64, 4, 5, per_op=True)
+    run("fused sampler (dpkn4), hid 64 / 4 heads / 5 layers", 64, 4, 5)
