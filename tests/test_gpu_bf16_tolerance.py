@@ -1,9 +1,10 @@
 """GPU tolerance study of the bf16 GEMM mode (BASELINE config 3: human36m_diffpose_uvxyz_gt eval,
 K=100 DDIM steps, T=101, bf16).  dpk_set_gemm_mode(h, 2) / HipGCNdiff.set_gemm_mode("bf16")
 rounds the operands of the per-layer GEMMs and (round 5) of attention's score and P.V products to bf16
-(8-bit mantissa) and accumulates in fp32; LayerNorm, the softmax, the graph products, the I/O ChebConvs
-and the DDIM update stay fp32.  (Round 5 measured the GraphNet products in bf16 as well: +1.1 % at
-30x the MPJPE delta, so they stay fp32; profiles/r05_bfag_check.txt.)
+(8-bit mantissa) and accumulates in fp32; the GraphNet products take bf16 X against L_g as a bf16 hi + lo
+pair (DPK_BF_GRAPH=2, two products, L_g to ~16 bits); LayerNorm, the softmax, the I/O ChebConvs and the
+DDIM update stay fp32.  (L_g rounded to bf16 alone measured +1.1 % at 30x the MPJPE delta, the hi + lo
+pair +1.4 % at 5.6x on 128 frames, 3.8e-4 -> 2.1e-3 mm: profiles/r05_bfag_check.txt, r05_ab_bg2.txt.)
 
 It is a reduced-precision mode, so it is NOT held to the fp32 bar (MPJPE delta <= 1e-4 mm).
 Measured on MI355X against the golden-pinned CPU oracle (tools/bf16_probe.py): one eps
