@@ -223,10 +223,11 @@ int dpk_gmm_sample_f64(const double* gmm_dev, const double* poses3d_dev, int n_s
  *   mode 1: 3-term fp16 split (a = a_hi + a_lo, w*64 = w_hi + w_lo; a_hi w_hi + a_hi w_lo +
  *           a_lo w_hi on v_mfma_f32_16x16x32_f16, fp32 accumulate), ~fp32-accurate products;
  *   mode 2: bf16 (a and w rounded to bf16, one v_mfma_f32_16x16x32_bf16 product, fp32
- *           accumulate; since round 5 also attention's score and P.V products): a reduced-precision
+ *           accumulate; since round 5 also attention's score and P.V products, and the GraphNet
+ *           products from bf16 activations against L_g as a bf16 hi + lo pair): a reduced-precision
  *           mode for the tolerance study of BASELINE config 3.
- * The input/output ChebConvs, LayerNorm, the softmax, the graph products and the DDIM update stay fp32
- * in all modes, and so does attention in modes 0 and 1.
+ * The input/output ChebConvs, LayerNorm, the softmax and the DDIM update stay fp32 in all modes, and
+ * so do attention and the GraphNet products in modes 0 and 1.
  * Applies to later dpk_sample / dpk_eps / dpk_pose calls on this handle.  Range: mode 1 needs
  * every GEMM weight |w| < 1015 (else those calls return DPK_E_UNSUPPORTED) and GEMM inputs
  * (LayerNorm/attention/graph/Chebyshev outputs) below 65504 in magnitude; an overflow there
