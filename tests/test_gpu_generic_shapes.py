@@ -1,13 +1,14 @@
 """GPU: GCNdiff / GCNpose at model shapes other than the compiled one (hid_dim 96, n_head 4,
-n_pts 17), which run on the generic-shape path (csrc/dpk_generic.inc).  The reference builds its
-models from any config (models/gcndiff.py:55-99, models/gcnpose.py:55-98); every config it ships
-uses the compiled shape (configs/human36m_*.yml:9-16), so there are no reference golden vectors at
-these shapes: the checker is the oracle, which issues the reference's ATen ops for any hid_dim,
-n_head and n_pts and is pinned bit-exact to the reference's goldens at the shipped shape
-(tests/test_oracle_golden.py) — parity here is pinned through the oracle, not by fixtures.
+n_pts 17), which run on the generic-shape path (csrc/dpk_generic.inc) — per-op launches, or for hid 128 /
+8 or 4 heads and hid 64 / 2 or 4 heads on 17 joints the persistent-sampler instances (dpk_genfused.inc).
+The reference builds its models from any config (models/gcndiff.py:55-99, models/gcnpose.py:55-98).
+Round 6: fixtures produced by the reference itself at five such shapes (tests/golden/g12_*, from
+tools/gen_goldens.py) pin both paths directly (test_shapes_vs_reference_goldens), and the oracle is
+bit-exact on them (tests/test_oracle_golden.py::test_other_shapes_vs_reference); the other tests here
+use the oracle as the checker on further inputs (per-pose masks, eta > 0, dense graphs, GCNpose).
 
 Tolerances as tests/test_gpu_parity.py: 5e-6 elementwise for eps and trajectories (fp32 sums in
-another order), MPJPE-style bars are not used (no targets at these shapes).
+another order).
 """
 import os
 from types import SimpleNamespace as ns
@@ -175,6 +176,8 @@ def test_generic_path_under_caller_capture(dev, monkeypatch, fused):
         m.sample(x, seq, _betas(), mask=ones)
         m(x, ones, t, 0)
     torch.cuda.current_stream(dev).wait_stream(s)
+    spare0 = m.debug_resources()["generic_spare_kib"]
+    assert spare0 > 0, "the uncaptured warm-up reserves the capture's scratch"
     out = torch.empty_like(x)
     out2 = torch.empty_like(x)
     eps = torch.empty_like(x)
@@ -199,7 +202,7 @@ def test_generic_path_under_caller_capture(dev, monkeypatch, fused):
     torch.cuda.synchronize(dev)
     m.sample(x, seq, _betas(), mask=ones)       # an uncaptured call recycles the capture's resources
     r = m.debug_resources()
-    assert r["released"] == 0 and r["generic_spare_mib"] >= 0
+    assert r["released"] == 0 and r["generic_spare_kib"] >= spare0   # the capture's scratch came back
     m.close()
 
 
@@ -395,4 +398,38 @@ def test_fused_wide_sampler_under_capture(dev, hid, heads):
         torch.cuda.synchronize(dev)
         assert torch.equal(out, eager)
     del g
+    m.close()
+
+
+G12 = ["g12_shape_h128_n8_l5_j17.npz", "g12_shape_h128_n4_l3_j17.npz", "g12_shape_h64_n2_l2_j17.npz",
+       "g12_shape_h64_n4_l5_j17.npz", "g12_shape_h48_n4_l1_j16.npz"]
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("name", G12)
+def test_shapes_vs_reference_goldens(dev, monkeypatch, golden, name, fused):
+    """Round 6: the other model shapes against fixtures produced by the reference itself at that
+    config.model (tools/gen_goldens.py g12; models/gcndiff.py:55-99, d_k = hid / n_head per
+    models/GraFormer.py:116-124): eps at 8 mixed t with the all-ones and a two-key mask, and the K=10
+    trajectory (xs, x0s) on 8 frames, at 5e-6.  fused "1": the 17-joint shapes run the persistent-sampler
+    instances (dpkw hid 128 / 8 heads, dpkw4 128 / 4, dpkn 64 / 2, dpkn4 64 / 4), the 16-joint chain the
+    per-op path; "0": every shape per-op.  The loop-graph count tells the two paths apart (the per-op path
+    records its K-step loop as a hipGraph, the fused instances are one launch)."""
+    g = golden(name)
+    hid, nh, nl, npts = int(g["hid"]), int(g["n_head"]), int(g["num_layer"]), int(g["n_pts"])
+    monkeypatch.setenv("DPK_GEN_FUSED", fused)
+    m = HipGCNdiff(g["adj"], _cfg(hid, nh, nl, npts), device=dev)
+    m.load_state_dict(synthetic_state_dict(hid=hid, n_layers=nl, n_pts=npts))
+    x, t = torch.from_numpy(g["x"]).to(dev), torch.from_numpy(g["t8"]).to(dev)
+    ones = torch.ones(1, 1, npts, dtype=torch.bool, device=dev)
+    assert record_delta(_maxdiff(m(x, ones, t, 0), torch.from_numpy(g["eps"])), TOL)
+    assert record_delta(_maxdiff(m(x, torch.from_numpy(g["mask2"]).to(dev), t, 0), torch.from_numpy(g["eps_masked"])), TOL)
+    xs, x0s = m.sample(x, [int(s) for s in g["seq"]], _betas(int(g["T"])), mask=ones, trajectory=True)
+    assert record_delta(_maxdiff(xs, torch.from_numpy(g["xs"])), TOL)
+    assert record_delta(_maxdiff(x0s, torch.from_numpy(g["x0s"])), TOL)
+    loops = m.debug_resources()["generic_loop_graphs"]
+    if fused == "1" and npts == 17:
+        assert loops == 0, "expected the fused persistent-sampler instance"
+    else:
+        assert loops >= 1, "expected the per-op path"
     m.close()

@@ -307,3 +307,36 @@ def test_draw_noise_sources():
         draw_noise(x, 2, ref)
     with pytest.raises(ValueError):
         draw_noise(x, 2, "gaussian")
+
+
+G12 = ["g12_shape_h128_n8_l5_j17.npz", "g12_shape_h128_n4_l3_j17.npz", "g12_shape_h64_n2_l2_j17.npz",
+       "g12_shape_h64_n4_l5_j17.npz", "g12_shape_h48_n4_l1_j16.npz"]
+
+
+@pytest.mark.parametrize("name", G12)
+def test_other_shapes_vs_reference(golden, name):
+    """Round 6: the oracle's shape-generic code (d_k 16 / 32 / 12, 2 / 8 heads, a 16-joint chain) pinned
+    bit-exact to the reference GCNdiff built at that config.model (models/gcndiff.py:55-99,
+    models/GraFormer.py:116-124; fixtures from tools/gen_goldens.py --only g12): eps with two masks and a
+    K=10 trajectory, with the build's generator weights at that shape (sha256 in meta.json)."""
+    import hashlib
+    g = golden(name)
+    hid, nh, nl, npts = int(g["hid"]), int(g["n_head"]), int(g["num_layer"]), int(g["n_pts"])
+    sd = synthetic_state_dict(hid=hid, n_layers=nl, n_pts=npts)
+    h = hashlib.sha256()
+    for k, v in sd.items():
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v, dtype="<f4").tobytes())
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    assert meta["shape_weights_sha256"][name[:-4]] == h.hexdigest()
+    P = O.params_to_torch(sd)
+    graph = O.adjacency(npts, [tuple(e) for e in g["edges"].tolist()])
+    assert np.array_equal(graph.numpy(), g["adj"])
+    ones = torch.ones(1, 1, npts, dtype=torch.bool)
+    x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["t8"])
+    fn = lambda xt, m, tt: O.gcndiff_forward(P, graph, xt, m, tt, n_layers=nl, heads=nh)  # noqa: E731
+    assert np.array_equal(fn(x, ones, t).numpy(), g["eps"])
+    assert np.array_equal(fn(x, torch.from_numpy(g["mask2"]), t).numpy(), g["eps_masked"])
+    xs, x0s = O.generalized_steps(x, ones, [int(s) for s in g["seq"]], fn, _betas(int(g["T"])))
+    assert np.array_equal(torch.stack(xs).numpy(), g["xs"])
+    assert np.array_equal(torch.stack(x0s).numpy(), g["x0s"])

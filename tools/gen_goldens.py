@@ -15,6 +15,7 @@ Usage:  python tools/gen_goldens.py [--ref /root/reference]
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -340,6 +341,51 @@ def main():
                  seed_hyber=12, out_hyber=xs_h[-1].numpy(),
                  seq50=np.array(seq50), eta50=np.float32(1.0), seed50=13, noise50=noise50.numpy(),
                  out50=xs50[-1].numpy())
+
+    # ---------------- G12: other model shapes (round 6) ----------------
+    # The reference builds GCNdiff from any config.model (models/gcndiff.py:55-99; d_k = hid / n_head,
+    # models/GraFormer.py:116-124): the shapes the build runs on its other persistent-sampler instances
+    # (hid 128 / 8 heads, 128 / 4, 64 / 2, 64 / 4 on the H36M graph) and on the per-op generic path
+    # (hid 48 / 4 heads on a 16-joint chain), each with the build's generator weights at that shape: eps at
+    # 8 mixed t with the all-ones and a two-key mask, and a K=10 trajectory on 8 frames.
+    if want("g12"):
+        chain16 = torch.tensor([[i, i + 1] for i in range(15)], dtype=torch.long)
+        shapes = [(128, 8, 5, 17, edges), (128, 4, 3, 17, edges), (64, 2, 2, 17, edges), (64, 4, 5, 17, edges),
+                  (48, 4, 1, 16, chain16)]
+        b51 = torch.from_numpy(get_beta_schedule("linear", beta_start=0.0001, beta_end=0.001,
+                                                 num_diffusion_timesteps=51)).float()
+        shas = {}
+        for hid, nh, nl, npts, ed in shapes:
+            scfg = types.SimpleNamespace(model=types.SimpleNamespace(
+                hid_dim=hid, emd_dim=hid, coords_dim=[5, 5], num_layer=nl, n_head=nh, dropout=0.25, n_pts=npts))
+            sadj = adj_mx_from_edges(num_pts=npts, edges=ed, sparse=False)
+            ssd = synthetic_state_dict(hid=hid, n_layers=nl, n_pts=npts)
+            sm = GCNdiff(sadj, scfg)
+            sm.load_state_dict({k: torch.from_numpy(v) for k, v in ssd.items()})
+            sm.eval()
+            smask = torch.tensor([[[True] * npts]])
+            smask2 = smask.clone()
+            smask2[0, 0, 2] = False
+            smask2[0, 0, npts - 1] = False
+            name = f"g12_shape_h{hid}_n{nh}_l{nl}_j{npts}"
+            x8, _ = synthetic_batch(8, seed=1200 + hid + nh, num_pts=npts)
+            x8 = torch.from_numpy(x8)
+            t8 = torch.tensor([49.0, 0.0, 12.0, 31.0, 7.0, 49.0, 25.0, 3.0])
+            with torch.no_grad():
+                eps = sm(x8, smask, t8, 0)
+                eps_masked = sm(x8, smask2, t8, 0)
+            seq10 = list(range(0, 50, 5))
+            xs, x0s = generalized_steps(x8, smask, seq10, sm, b51, eta=0.0)
+            np.savez(os.path.join(args.out, name + ".npz"), hid=hid, n_head=nh, num_layer=nl, n_pts=npts,
+                     edges=ed.numpy(), adj=sadj.numpy(), x=x8.numpy(), t8=t8.numpy(), eps=eps.numpy(),
+                     mask2=smask2.numpy(), eps_masked=eps_masked.numpy(), seq=np.array(seq10), T=51,
+                     xs=torch.stack(xs).numpy(), x0s=torch.stack(x0s).numpy())
+            hh = hashlib.sha256()
+            for k_, v_ in ssd.items():        # the generator's layout order at this shape
+                hh.update(k_.encode())
+                hh.update(np.ascontiguousarray(v_, dtype="<f4").tobytes())
+            shas[name] = hh.hexdigest()
+        meta["shape_weights_sha256"] = shas
 
     with open(os.path.join(args.out, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
