@@ -25,7 +25,10 @@ still advances torch's RNG by K draws there; ``noise="torch"`` reproduces that t
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
+
 import torch
 
 from .gcndiff import HipGCNdiff
@@ -94,22 +97,41 @@ def generalized_steps(x, src_mask, seq, model, b, **kwargs):
 # One schedule-only DDIM handle per (device, thread), reused by every generic-callable call: the
 # reference's sampler allocates nothing persistent (common/utils_diff.py:46-68), so neither should
 # a call here (a handle costs dpk_create, device buffers and a schedule upload).  A handle serves one
-# thread (include/diffpose_kernels.h), hence the thread in the key.
-_SCHED_HANDLES: dict = {}
+# thread (include/diffpose_kernels.h), so the cache is thread-local: a thread's handles are destroyed
+# with its thread-local storage when it exits (HipGCNdiff.__del__), and clear_schedule_handles() closes
+# the calling thread's handles at once (a thread pool no longer keeps one handle per thread it
+# ever ran until the process ends).
+_SCHED_TLS = threading.local()
+
+
+def _sched_cache() -> dict:
+    c = getattr(_SCHED_TLS, "handles", None)
+    if c is None:
+        c = _SCHED_TLS.handles = {}
+    return c
 
 
 def schedule_handle(device) -> HipGCNdiff:
     """The cached schedule-only handle of ``device`` for the calling thread (created on first use)."""
-    import threading
-
     dev = torch.device(device)
-    key = (dev.type, dev.index or 0, threading.get_ident())
-    upd = _SCHED_HANDLES.get(key)
+    key = (dev.type, dev.index or 0)
+    cache = _sched_cache()
+    upd = cache.get(key)
     if upd is None:
         upd = HipGCNdiff.__new__(HipGCNdiff)
         _init_schedule_only(upd, dev)
-        _SCHED_HANDLES[key] = upd
+        cache[key] = upd
     return upd
+
+
+def clear_schedule_handles() -> int:
+    """Close the calling thread's cached schedule-only handles; returns how many were closed."""
+    cache = _sched_cache()
+    n = len(cache)
+    for upd in cache.values():
+        upd.close()
+    cache.clear()
+    return n
 
 
 def _init_schedule_only(obj: HipGCNdiff, device) -> None:

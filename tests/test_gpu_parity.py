@@ -124,13 +124,23 @@ def test_generic_callable_path(model, mask):
     # the schedule-only DDIM handle is created once per device and reused: a second call (another
     # schedule) allocates no new handle, and the first call's results come back unchanged after it
     h1 = utils_diff.schedule_handle(x.device)
-    n_handles = len(utils_diff._SCHED_HANDLES)
+    n_handles = len(utils_diff._sched_cache())
     seq2 = make_seq("uniform", 50, 5)
     utils_diff.generalized_steps(x, mask, seq2, lambda a, m, t, c: model(a, m, t, c), _betas(51).cuda())
     again_xs, _ = utils_diff.generalized_steps(x, mask, seq, lambda a, m, t, c: model(a, m, t, c), _betas(51).cuda())
-    assert utils_diff.schedule_handle(x.device) is h1 and len(utils_diff._SCHED_HANDLES) == n_handles
+    assert utils_diff.schedule_handle(x.device) is h1 and len(utils_diff._sched_cache()) == n_handles
     assert h1._h.value == utils_diff.schedule_handle(x.device)._h.value
     assert torch.equal(torch.stack(again_xs), torch.stack(gen_xs))
+    # the cache is per thread; another thread gets its own handle, and
+    # clear_schedule_handles() closes the calling thread's handles
+    import threading
+    other = []
+    th = threading.Thread(target=lambda: other.append(utils_diff.schedule_handle(x.device)._h.value))
+    th.start()
+    th.join()
+    assert other and other[0] != h1._h.value
+    assert utils_diff.clear_schedule_handles() == n_handles and h1._h is None
+    assert utils_diff.schedule_handle(x.device) is not h1
 
 
 @pytest.mark.parametrize("n", [1, 3, 5, 67])
