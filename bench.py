@@ -91,6 +91,8 @@ def parse(argv=None):
                     help="frames of the CPU baseline and parity sample (default: rank 0's whole batch, at most "
                          "1024 rows, i.e. 1024 // H frames)")
     ap.add_argument("--cpu-repeats", type=int, default=3)
+    ap.add_argument("--c3-frames", type=int, default=256,
+                    help="frames of the config-3 (bf16, K=100) variant's parity study against the oracle")
     ap.add_argument("--cpu-threads", type=str, default=None,
                     help="comma-separated thread counts for the CPU baseline legs (default: the box's CPU share, "
                          "OMP_NUM_THREADS, or every physical core of this process's affinity when unset)")
@@ -253,6 +255,41 @@ def cpu_baseline(args, x_all, seq, betas, K, hyp):
     return res, (ref.numpy() if ref is not None else None), n_cpu
 
 
+def config3_parity(args, x_all, tgt_all, out_bf16, out_fp32):
+    """BASELINE config 3's tolerance study: the oracle (reference op order, torch CPU fp32) at K=100 over T=101 on
+    the first --c3-frames frames; MPJPE delta and max |diff| of the bf16 run and, on the same frames, of the fp32
+    mode (same schedule), against it.  bf16 is a study, not held to the fp32 bar of 1e-4 mm."""
+    import numpy as np
+    import torch
+
+    from diffpose_amd.schedule import get_beta_schedule, make_seq
+    from diffpose_amd.weights import synthetic_state_dict
+    from oracle import gcndiff_oracle as O
+
+    n = min(args.c3_frames, x_all.shape[0])
+    seq3 = make_seq("uniform", CONFIGS[3]["T_test"], CONFIGS[3]["K"])
+    b3 = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
+                                            num_diffusion_timesteps=CONFIGS[3]["T"])).float()
+    P = O.params_to_torch(synthetic_state_dict())
+    adj = O.adjacency()
+    mask = torch.ones(1, 1, 17, dtype=torch.bool)
+    t0 = time.perf_counter()
+    xs, _ = O.generalized_steps(torch.from_numpy(x_all[:n]), mask, seq3,
+                                lambda a, m, t: O.gcndiff_forward(P, adj, a, m, t), b3, eta=0.0)
+    cpu_s = time.perf_counter() - t0
+    ref = xs[-1].numpy()
+    tg = tgt_all[:n]
+    m_r = mpjpe_mm(ref, tg, 1)
+    res = {"frames": n, "K": len(seq3), "T": CONFIGS[3]["T"], "mpjpe_ref_mm": round(m_r, 6), "oracle_s": round(cpu_s, 2),
+           "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs and of attention's score and "
+                   "P.V products; fp32 beside it on the same frames and schedule; the fp32 bar is 1e-4 mm"}
+    for name, o in (("bf16", out_bf16), ("fp32", out_fp32)):
+        m_h = mpjpe_mm(o[:n], tg, 1)
+        res[name] = {"mpjpe_hip_mm": round(m_h, 6), "mpjpe_delta_mm": float(f"{abs(m_h - m_r):.3e}"),
+                     "max_abs_diff": float(f"{float(np.abs(o[:n] - ref).max()):.3e}")}
+    return res
+
+
 # ---------------------------------------------------------------------------------------------
 # one rank
 # ---------------------------------------------------------------------------------------------
@@ -335,11 +372,13 @@ def rank_main(args):
                                 torch.full((hi - lo,), float("nan"), dtype=torch.float64)], dim=1)
         return torch.stack(pose_errors(o, tg_local, args.hyp, root_mode="relative"), dim=1)
 
+    cur = {"seq": seq, "betas": betas}         # the schedule step() runs (the config-3 variant swaps it)
+
     def step():
         if dry:
             torch.mul(x, 2.0, out=out)                 # stand-in for the sampler: rank-independent, exact
         else:
-            model.sample(x, seq, betas, eta=args.eta, out=out)
+            model.sample(x, cur["seq"], cur["betas"], eta=args.eta, out=out)
         # the final MPJPE reduction (north_star) at every N, N=1 included, so every point of the scaling
         # sweep times the same work: per-frame errors of this rank's frames (dpk_pose_metrics), and under
         # a launcher the one data-path collective, their all-gather (16 B per frame)
@@ -385,7 +424,7 @@ def rank_main(args):
             model.profile(False)
         return elapsed, mine, kernel_ms
 
-    def roofline(gemm, kernel_ms):
+    def roofline(gemm, kernel_ms, K=K):
         if not kernel_ms:
             return None
         km = np.asarray(kernel_ms, dtype=np.float64)
@@ -491,6 +530,26 @@ def rank_main(args):
                            "dtype": DTYPES[g]}
             if world == 1 and rank == 0:
                 variants[g]["_out"] = out.detach().cpu().numpy()
+        # BASELINE config 3 (human36m_diffpose_uvxyz_gt: K=100 over T'=100, T=101, bf16 tolerance study) on the
+        # same frames, on the driver's line since round 6: its own roofline (dense bf16 peak) and, on rank 0 at
+        # N=1, a parity study against the oracle (below)
+        if args.config == 2 and args.hyp == 1:
+            seq3 = make_seq("uniform", CONFIGS[3]["T_test"], CONFIGS[3]["K"])
+            b3 = torch.from_numpy(get_beta_schedule("linear", beta_start=1e-4, beta_end=1e-3,
+                                                    num_diffusion_timesteps=CONFIGS[3]["T"])).float()
+            cur.update(seq=seq3, betas=b3)
+            e3, _, k3 = measure("bf16")
+            variants["config3_bf16"] = {
+                "value": round(B_total * args.steps / e3, 2), "ms_per_step": round(e3 / args.steps * 1e3, 4),
+                "roofline": roofline("bf16", k3, K=len(seq3)), "dtype": DTYPES["bf16"],
+                "workload": (f"BASELINE config 3: {CONFIGS[3]['yml']} eval, {B_total} frames, K={len(seq3)} DDIM "
+                             f"(uniform skip over T'={CONFIGS[3]['T_test']}, T={CONFIGS[3]['T']}), bf16 layer GEMMs")}
+            if world == 1 and rank == 0:
+                variants["config3_bf16"]["_out"] = out.detach().cpu().numpy()
+                model.set_gemm_mode("fp32")            # the fp32 mode on the same schedule, for the parity study
+                model.sample(x, seq3, b3, eta=args.eta, out=out)
+                variants["config3_bf16"]["_out_fp32"] = out.detach().cpu().numpy()
+            cur.update(seq=seq, betas=betas)
         model.set_gemm_mode(args.gemm)
 
     frames_done = B_total * args.steps
@@ -560,9 +619,14 @@ def rank_main(args):
                 return r
             result["parity"] = parity(out_main, args.gemm)
             for g, v in variants.items():
-                v["parity"] = parity(v["_out"], g)
+                if g in ("fp32", "f16x3"):
+                    v["parity"] = parity(v["_out"], g)
+        c3 = variants.get("config3_bf16")
+        if c3 is not None and args.eta == 0.0:
+            c3["parity"] = config3_parity(args, x_all, tgt_all, c3["_out"], c3["_out_fp32"])
     for v in variants.values():
         v.pop("_out", None)
+        v.pop("_out_fp32", None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if use_dist:
