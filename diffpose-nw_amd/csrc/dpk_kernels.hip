@@ -65,15 +65,6 @@ __device__ __forceinline__ void tr_stamp() {
 #ifndef DPK_GEMM_HOOK
 #define DPK_GEMM_HOOK(tag)
 #endif
-#ifndef DPK_SPLIT_NOINLINE
-#define DPK_SPLIT_NOINLINE 0   // A/B: the step-split handoff as called functions
-#endif
-#ifndef DPK_ZM0_PHILOX
-#define DPK_ZM0_PHILOX 1   // eta != 0 without a noise buffer stays in the ZM = 0 kernel (the round-3 code)
-#endif
-#ifndef DPK_EXP
-#define DPK_EXP 0      // timing experiments: 1 = GEMM epilogue dropped (acc kept live), 2 = wave 3 idle in GEMMs
-#endif
 
 
 // Launch arguments of the sampler kernel, shared by both tile sizes (dpk_sampler.inc).
@@ -168,33 +159,6 @@ namespace dpkn4 {
 #undef DPK_NH
 #undef DPK_D
 #undef DPK_P
-// Measured-slower tile variants for the half-width-operand GEMM modes, built only
-// with -DDPK_EXPT_TILES=1 (tools/build_variant.sh) and selected at handle creation by DPK_CORES=1 / DPK_W8=1:
-//  * 2-pose tiles built for two workgroups per CU (the half-width MFMAs leave the SIMD free for the other
-//    workgroup's VALU work): bf16 config 3 107.3k vs 115.3k poses/s, f16x3 116k vs 153k (49 VGPRs spilled);
-//  * 4-pose tiles on 8 waves, two per SIMD: 223 VGPRs spilled under the 256-register budget, 2.1x slower.
-#ifndef DPK_EXPT_TILES
-#define DPK_EXPT_TILES 0
-#endif
-#if DPK_EXPT_TILES
-#define DPK_P 2
-#undef DPK_WGCU
-#define DPK_WGCU 2
-namespace dpk2c {
-#include "dpk_sampler.inc"
-}  // namespace dpk2c
-#undef DPK_WGCU
-#undef DPK_P
-// 4-pose tiles on 8 waves, two per SIMD (gemm modes 1, 2: launch_tiles, DPK_W8)
-#define DPK_P 4
-#undef DPK_NW
-#define DPK_NW 8
-namespace dpk8 {
-#include "dpk_sampler.inc"
-}  // namespace dpk8
-#undef DPK_NW
-#undef DPK_P
-#endif  // DPK_EXPT_TILES
 
 namespace dpk {
 
@@ -295,8 +259,6 @@ struct dpk_handle {
     int num_layers = NL;           // config num_layer (1..NL): layers the kernels run
     int n_cu = 256;                // compute units of the device (workgroups per round)
     int tail_plan = 2;             // dpk_set_tail_plan: 0 4-pose tiles, 1 2-pose tail round, 2 step split
-    bool coresident = false;       // gemm modes 1, 2: 2-pose tiles, two workgroups per CU (DPK_CORES=1)
-    bool w8 = false;               // gemm modes 1, 2: 4-pose tiles on 8 waves (DPK_W8=1)
     unsigned* flags = nullptr;     // device: FLAG_SLOTS x n_cu step-split handoff words (zero between launches),
                                    // then the split fallback counter
     std::vector<int> slot_free;    // flag slots no launch holds
@@ -529,16 +491,17 @@ static bool drain_relaxed() {
     return se == hipSuccess;
 }
 
-// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  No drain: the release
-// callback runs when the graph's executable is destroyed, and on this runtime destroying an executable
-// waits for its launches in flight (tools/probe_user_object_release.py: deleting a CUDAGraph 0.1 ms after
-// its 175 ms replay was enqueued returned when the replay had finished, and `released` was never seen
-// set while it ran), so nothing the capture reads is still in use.  (Round 4 drained the device here;
-// from another thread during a global-mode capture that invalidated the capture, advisor r04.)
+// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  The release callback
+// runs when the graph's executable is destroyed; on this runtime that destruction waits for its launches
+// in flight (tools/probe_user_object_release.py), but the recycling does not rely on it: when a
+// release is pending the device is drained first, in relaxed capture mode so that another thread's
+// global-mode capture is not invalidated (advisor r04), and when the runtime refuses the sync (a stream of
+// the device is capturing) the recycling is put off to a later call.
 static void cap_sweep(dpk_handle* h) {
     bool any = false;
     for (CapRes* c : h->caps) any = any || (c->tracked && c->released.load());
     if (!any) return;
+    if (!drain_relaxed()) return;
     std::vector<CapRes*> keep;
     for (CapRes* c : h->caps) {
         if (!(c->tracked && c->released.load())) {
@@ -692,41 +655,17 @@ static void launch_tiles(dpk_handle* h, int blocks, size_t shmem, hipStream_t st
 #define DPK_LAUNCH(NS)                                                                                          \
     do {                                                                                                        \
         if constexpr (MODE == M_SAMPLE) {                                                                       \
-            if (a.noise || (!DPK_ZM0_PHILOX && a.eta != 0.f)) {                                                 \
-                if (a.noise && h->sparse_graph) DPK_LAUNCH3(NS, true, 1);                                       \
-                else if (a.noise) DPK_LAUNCH3(NS, false, 1);                                                    \
-                else if (h->sparse_graph) DPK_LAUNCH3(NS, true, 2);                                             \
-                else DPK_LAUNCH3(NS, false, 2);                                                                 \
+            if (a.noise) {      /* the caller's draws (ZM = 1) */                                               \
+                if (h->sparse_graph) DPK_LAUNCH3(NS, true, 1);                                                  \
+                else DPK_LAUNCH3(NS, false, 1);                                                                 \
                 break;                                                                                          \
             }                                                                                                   \
         }                                                                                                       \
         if (h->sparse_graph) DPK_LAUNCH3(NS, true, 0);                                                          \
         else DPK_LAUNCH3(NS, false, 0);                                                                         \
     } while (0)
-    if constexpr (PT == 4) {
-        if (DPK_EXPT_TILES && h->w8 && gm != 0) {
-#if DPK_EXPT_TILES
-            // 8-wave 4-pose tiles: only the half-width-operand GEMM modes are instantiated
-            const dim3 block8(dpk8::NT);
-#define DPK_LAUNCH8(SP, NZ)                                                                                          \
-    do {                                                                                                           \
-        if (gm == 1) hipLaunchKernelGGL((dpk8::sample_kernel<MODE, SP, 1, NZ>), grid, block8, shmem, st, a, h->arena, a16); \
-        else hipLaunchKernelGGL((dpk8::sample_kernel<MODE, SP, 2, NZ>), grid, block8, shmem, st, a, h->arena, a16);       \
-    } while (0)
-            const int nz = (MODE == M_SAMPLE && a.noise) ? 1 : (MODE == M_SAMPLE && !DPK_ZM0_PHILOX && a.eta != 0.f) ? 2 : 0;
-            if (h->sparse_graph) {
-                if (nz == 1) DPK_LAUNCH8(true, 1); else if (nz == 2) DPK_LAUNCH8(true, 2); else DPK_LAUNCH8(true, 0);
-            } else {
-                if (nz == 1) DPK_LAUNCH8(false, 1); else if (nz == 2) DPK_LAUNCH8(false, 2); else DPK_LAUNCH8(false, 0);
-            }
-#undef DPK_LAUNCH8
-            return;
-#endif
-        }
-        DPK_LAUNCH(dpk);
-    } else {
-        DPK_LAUNCH(dpk2);
-    }
+    if constexpr (PT == 4) DPK_LAUNCH(dpk);
+    else DPK_LAUNCH(dpk2);
 #undef DPK_LAUNCH
 #undef DPK_LAUNCH3
 }
@@ -748,28 +687,6 @@ template <int MODE>
 static int launch_sampler(dpk_handle* h, hipStream_t st, SampleArgs a, bool cap) {
     const int N = a.N;
     const int round4 = P * h->n_cu;
-    if constexpr (MODE == M_SAMPLE) {
-        // co-resident 2-pose tiles, two workgroups per CU (gemm modes 1, 2; DPK_CORES=1)
-        if (DPK_EXPT_TILES && h->coresident && h->gemm_mode != 0) {
-#if DPK_EXPT_TILES
-            a.pose_off = 0;
-            const dim3 grid((N + 1) / 2), block(NT);
-            const char* a16 = h->gemm_mode == 2 ? h->arenabf : h->arena16;
-#define DPK_LAUNCH_C(SP, G, NZ) hipLaunchKernelGGL((dpk2c::sample_kernel<MODE, SP, G, NZ>), grid, block, 0, st, a, h->arena, a16)
-            const int nz = a.noise ? 1 : (!DPK_ZM0_PHILOX && a.eta != 0.f) ? 2 : 0;
-            if (h->sparse_graph) {
-                if (h->gemm_mode == 1) { if (nz == 1) DPK_LAUNCH_C(true, 1, 1); else if (nz == 2) DPK_LAUNCH_C(true, 1, 2); else DPK_LAUNCH_C(true, 1, 0); }
-                else { if (nz == 1) DPK_LAUNCH_C(true, 2, 1); else if (nz == 2) DPK_LAUNCH_C(true, 2, 2); else DPK_LAUNCH_C(true, 2, 0); }
-            } else {
-                if (h->gemm_mode == 1) { if (nz == 1) DPK_LAUNCH_C(false, 1, 1); else if (nz == 2) DPK_LAUNCH_C(false, 1, 2); else DPK_LAUNCH_C(false, 1, 0); }
-                else { if (nz == 1) DPK_LAUNCH_C(false, 2, 1); else if (nz == 2) DPK_LAUNCH_C(false, 2, 2); else DPK_LAUNCH_C(false, 2, 0); }
-            }
-#undef DPK_LAUNCH_C
-            HIPCHK(h, hipGetLastError());
-            return DPK_OK;
-#endif
-        }
-    }
     if constexpr (MODE == M_SAMPLE) {
         const int tiles = (N + P - 1) / P, q = tiles / h->n_cu, r = tiles % h->n_cu;
         if (h->tail_plan == 2 && a.K >= 2 && q >= 1 && r > 0 && 2 * r <= h->n_cu) {
@@ -863,8 +780,6 @@ int dpk_create(const dpk_config* cfg, dpk_handle** out) {
     h->n_cu = std::max(h->n_cu, 1);
     // DPK_TAIL_SPLIT=0/1/2: the initial tail plan (A/B timing); trace builds stamp per block id
     if (const char* ts = getenv("DPK_TAIL_SPLIT")) h->tail_plan = std::min(std::max(atoi(ts), 0), 2);
-    if (const char* cr = getenv("DPK_CORES")) h->coresident = atoi(cr) != 0;
-    if (const char* w8 = getenv("DPK_W8")) h->w8 = atoi(w8) != 0 && !DPK_TRACE;
     if (DPK_TRACE) h->tail_plan = 0;
     // FLAG_SLOTS x n_cu handoff words + the fallback counter
     const size_t flag_bytes = ((size_t)FLAG_SLOTS * h->n_cu + 4) * 4;
@@ -1065,10 +980,9 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
             const float* w = n < D ? wq : (n < 2 * D ? wk : wv);
             return w[(n % D) * D + k];
         };
-        // fp32 QKV GEMM with LN0's affine folded in (DPK_LN0_FOLD; the LN phase writes
-        // (x - mean) / (std + eps)): W' = diag(a) W, bias c = b W + b_qkv (summed in double)
-        const bool fold0 = DPK_LN0_FOLD && !DPK_LN_FUSE;
-        pack_blocks(Lw + OFF_QKV, D, D3, KB_D, 18, [&](int k, int n) { return fold0 ? n0a[k] * wqkv(k, n) : wqkv(k, n); });
+        // QKV GEMM with LN0's affine folded in (the LN phase writes (x - mean) / (std + eps)):
+        // W' = diag(a) W, bias c = b W + b_qkv (summed in double)
+        pack_blocks(Lw + OFF_QKV, D, D3, KB_D, 18, [&](int k, int n) { return n0a[k] * wqkv(k, n); });
         for (int n = 0; n < D3; ++n) {
             double cs = 0.0;
             for (int k = 0; k < D; ++k) cs += (double)n0b[k] * (double)wqkv(k, n);
@@ -1084,7 +998,7 @@ int dpk_load_weights(dpk_handle* h, const char* const* names, const float* const
         pack_blocks(Lw + OFF_C2, D3, D, KB_D3, 6, [&](int k, int n) { return c2w[k * D + n]; });
         // the half-width-operand GEMMs (modes 1, 2) read the fp32 mode's operands: LN0 folded into QKV
         // (bias OFF_CQKV), the Chebyshev GEMMs' [x | T1x | T2x] in the reference's row order
-        auto wqkv_f = [&](int k, int n) { return fold0 ? n0a[k] * wqkv(k, n) : wqkv(k, n); };
+        auto wqkv_f = [&](int k, int n) { return n0a[k] * wqkv(k, n); };
         auto wo_f = [&](int k, int n) { return wo[n * D + k]; };
         auto f1_f = [&](int k, int n) { return f1w[n * D + k]; };
         auto f2_f = [&](int k, int n) { return f2w[n * D2 + k]; };
@@ -1534,7 +1448,7 @@ int dpk_debug_resources(dpk_handle* h, int* out, int n) {
         released += (c->tracked && c->released.load()) ? 1 : 0;
     }
     const int v[8] = {(int)h->caps.size(), tracked, released, (int)h->slot_free.size(), retired,
-                      h->eps_spare.cap, gen_graph_count(h->gen), gen_spare_mib(h->gen)};
+                      h->eps_spare.cap, gen_graph_count(h->gen), gen_spare_kib(h->gen)};
     for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
     return DPK_OK;
 }

@@ -227,7 +227,7 @@ class _HipModel:
         buf = (ctypes.c_int * 8)()
         _lib.check(self._h, "dpk_debug_resources", _lib.lib().dpk_debug_resources(self._h, buf, 8))
         keys = ("captures", "tracked", "released", "free_slots", "retired_schedules", "eps_spare_poses",
-                "generic_loop_graphs", "generic_spare_mib")
+                "generic_loop_graphs", "generic_spare_kib")
         return dict(zip(keys, list(buf)))
 
     def profile(self, enable: bool = True) -> None:

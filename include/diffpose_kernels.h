@@ -268,7 +268,7 @@ int dpk_profile_read(dpk_handle* h, float* ms_out, int cap, int* count);
  * dpk_debug_resources: out[0..7] = captures holding resources, captures whose graph holds our
  * user object, captures released (graph gone, not yet recycled), free flag slots, retired
  * schedules, spare dpk_eps capacity (poses); generic-shape handles also: K-step loops recorded as
- * hipGraphs (out[6]) and the spare capture scratch in MiB (out[7]). */
+ * hipGraphs (out[6]) and the spare capture scratch in KiB (out[7]). */
 int dpk_debug_split(dpk_handle* h, int mode, int* fallbacks);
 int dpk_debug_resources(dpk_handle* h, int* out, int n);
 

@@ -20,10 +20,12 @@ def main():
     ap.add_argument("func")
     ap.add_argument("--kernel", default="_ZN3dpk13sample_kernelILi0ELb1ELi0EE")
     ap.add_argument("--nth", type=int, default=0, help="which marked region inside the kernel")
+    ap.add_argument("--ignore-returns", action="store_true",
+                    help="no end marker at early returns (a never-taken guard such as attention's pose >= P)")
     a = ap.parse_args()
     s = open(SRC).read()
     i = s.index(f"__device__ __forceinline__ void {a.func}(")
-    b = s.index("{", i)
+    b = s.index(") {", i) + 2   # the body (not a default argument such as Hook{})
     # matching closing brace
     depth, j = 0, b
     while True:
@@ -35,11 +37,14 @@ def main():
                 break
         j += 1
     body = s[b + 1:j]
-    s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN" ::: "memory");' + body.replace("return;", 'asm volatile(";MARK_END" ::: "memory"); return;') \
+    s2 = s[:b + 1] + '\n    asm volatile(";MARK_BEGIN" ::: "memory");' + (body if a.ignore_returns else body.replace("return;", 'asm volatile(";MARK_END" ::: "memory"); return;')) \
         + '    asm volatile(";MARK_END" ::: "memory");\n' + s[j:]
     # the device functions live in dpk_sampler.inc, included by dpk_kernels.hip: compile a copy of
     # both from a scratch directory
     os.makedirs("/tmp/isa_count", exist_ok=True)
+    for inc in os.listdir(os.path.dirname(SRC)):
+        if inc.endswith(".inc"):
+            open(os.path.join("/tmp/isa_count", inc), "w").write(open(os.path.join(os.path.dirname(SRC), inc)).read())
     open("/tmp/isa_count/dpk_sampler.inc", "w").write(s2)
     tmp = "/tmp/isa_count/dpk_kernels.hip"
     open(tmp, "w").write(open(KSRC).read())
