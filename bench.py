@@ -91,7 +91,7 @@ def parse(argv=None):
                     help="frames of the CPU baseline and parity sample (default: rank 0's whole batch, at most "
                          "1024 rows, i.e. 1024 // H frames)")
     ap.add_argument("--cpu-repeats", type=int, default=3)
-    ap.add_argument("--c3-frames", type=int, default=256,
+    ap.add_argument("--c3-frames", type=int, default=1024,
                     help="frames of the config-3 (bf16, K=100) variant's parity study against the oracle")
     ap.add_argument("--cpu-threads", type=str, default=None,
                     help="comma-separated thread counts for the CPU baseline legs (default: the box's CPU share, "

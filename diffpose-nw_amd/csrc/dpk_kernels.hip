@@ -491,17 +491,18 @@ static bool drain_relaxed() {
     return se == hipSuccess;
 }
 
-// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  The release callback
-// runs when the graph's executable is destroyed; on this runtime that destruction waits for its launches
-// in flight (tools/probe_user_object_release.py), but the recycling does not rely on it: when a
-// release is pending the device is drained first, in relaxed capture mode so that another thread's
-// global-mode capture is not invalidated (advisor r04), and when the runtime refuses the sync (a stream of
-// the device is capturing) the recycling is put off to a later call.
+// Uncaptured calls only: recycle the resources of captures whose graphs are gone.  No drain: the release
+// callback runs when the graph's executable is destroyed, and on this runtime destroying an executable
+// waits for its launches in flight (tools/probe_user_object_release.py: deleting a CUDAGraph 0.1 ms after
+// its 175 ms replay was enqueued returned when the replay had finished, and `released` was never seen
+// set while it ran), so nothing the capture reads is still in use.  A drain here, even in relaxed capture
+// mode, invalidates another thread's global-mode capture on this runtime (round 4 without the relaxed
+// mode, advisor r04; round 6 with it, ADVICE r05: test_sweep_while_another_thread_captures failed with
+// hipErrorStreamCaptureInvalidated), so the recycling relies on that blocking destruction.
 static void cap_sweep(dpk_handle* h) {
     bool any = false;
     for (CapRes* c : h->caps) any = any || (c->tracked && c->released.load());
     if (!any) return;
-    if (!drain_relaxed()) return;
     std::vector<CapRes*> keep;
     for (CapRes* c : h->caps) {
         if (!(c->tracked && c->released.load())) {

@@ -414,7 +414,7 @@ def test_shapes_vs_reference_goldens(dev, monkeypatch, golden, name, fused):
     trajectory (xs, x0s) on 8 frames, at 5e-6.  fused "1": the 17-joint shapes run the persistent-sampler
     instances (dpkw hid 128 / 8 heads, dpkw4 128 / 4, dpkn 64 / 2, dpkn4 64 / 4), the 16-joint chain the
     per-op path; "0": every shape per-op.  The loop-graph count tells the two paths apart (the per-op path
-    records its K-step loop as a hipGraph, the fused instances are one launch)."""
+    records its K-step loop as a hipGraph when no trajectory is asked for, the fused instances are one launch)."""
     g = golden(name)
     hid, nh, nl, npts = int(g["hid"]), int(g["n_head"]), int(g["num_layer"]), int(g["n_pts"])
     monkeypatch.setenv("DPK_GEN_FUSED", fused)
@@ -427,6 +427,9 @@ def test_shapes_vs_reference_goldens(dev, monkeypatch, golden, name, fused):
     xs, x0s = m.sample(x, [int(s) for s in g["seq"]], _betas(int(g["T"])), mask=ones, trajectory=True)
     assert record_delta(_maxdiff(xs, torch.from_numpy(g["xs"])), TOL)
     assert record_delta(_maxdiff(x0s, torch.from_numpy(g["x0s"])), TOL)
+    # the final alone (no trajectory: the per-op path records its loop as a hipGraph) equals the trajectory's
+    out = m.sample(x, [int(s) for s in g["seq"]], _betas(int(g["T"])), mask=ones)
+    assert torch.equal(out, xs[-1])
     loops = m.debug_resources()["generic_loop_graphs"]
     if fused == "1" and npts == 17:
         assert loops == 0, "expected the fused persistent-sampler instance"

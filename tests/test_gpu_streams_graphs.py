@@ -430,10 +430,12 @@ def test_capture_resources_follow_the_graph(dev, monkeypatch):
 
 
 def test_sweep_while_another_thread_captures(dev, monkeypatch):
-    """advisor r04: handle B's uncaptured dpk_sample recycles a released capture's resources (a device
-    drain, cap_sweep) while thread A holds a global-mode capture open (torch.cuda.graph's default) on
-    handle A.  The drain runs in relaxed capture mode, or is put off to a later call when the runtime
-    refuses it: A's capture must complete and replay bitwise, and B's launch gives the eager result."""
+    """advisor r04: handle B's uncaptured dpk_sample recycles a released capture's resources (cap_sweep)
+    while thread A holds a global-mode capture open (torch.cuda.graph's default) on handle A.  cap_sweep
+    does not drain the device (a hipDeviceSynchronize there, even in relaxed capture mode, invalidates A's
+    capture on this runtime: round 6 measured it); it relies on graph destruction waiting for in-flight
+    replays (tools/probe_user_object_release.py).  A's capture must complete and replay bitwise, and B's
+    launch gives the eager result."""
     import gc
     import threading
     import time
@@ -498,7 +500,8 @@ def test_sweep_while_another_thread_captures(dev, monkeypatch):
     gA.replay()
     torch.cuda.synchronize()
     assert torch.equal(outA, eager)
-    mB.sample(x, seq, _betas(), mask=mask)       # a later call recycles the release if the first was refused
+    assert mB.debug_resources()["released"] == 0     # B's call recycled the release
+    mB.sample(x, seq, _betas(), mask=mask)
     assert mB.debug_resources()["released"] == 0
     del gA
     mA.close()

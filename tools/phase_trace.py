@@ -22,13 +22,10 @@ SO = os.environ.get("DPK_TRACE_SO", os.path.join(ROOT, "build", "trace", "libdpk
 # stamp sequence of one DDIM step: every workgroup barrier stamps before ("pre") and after
 # ("post"); every gemm_wave stamps at the end of its k-loop ("loop") and of its epilogue ("epi")
 # the f16x3 GEMMs run a wave's column tiles in passes and stamp per pass
-def _events(gemm_mode="fp32", fused=None):
-    # fp32 mode built with -DDPK_LN_FUSE=1: no LayerNorm phases (LN0 in the QKV operand, LN1 in graph1)
-    if fused is None:
-        fused = gemm_mode == "fp32" and os.environ.get("DPK_LN_FUSE", "0") == "1"
-    # LN1 mapped wave = pose (DPK_LN1_POSE, the default; every GEMM mode since round 5): no barrier
-    # between LN1 and graph1
-    ln1pose = not fused and os.environ.get("DPK_LN1_POSE", "1") == "1"
+def _events(gemm_mode="fp32"):
+    # LN1 is mapped wave = pose in 4-pose tiles: no barrier between LN1 and graph1 (round 6 removed the
+    # fused-LayerNorm builds, which had no LN phases)
+    fused, ln1pose = False, True
     ev = []
     bar = lambda n: ev.extend([(n, "pre"), (n, "post")])
     # the half-width-operand GEMMs run a wave's column tiles in passes (gemmh_wg): f16x3 QKV 3 x 3 tiles,
