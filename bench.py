@@ -53,7 +53,8 @@ PEAK_FP32_MFMA = 157.3      # TFLOP/s, MI355X FP32 matrix peak (MI355X_MICROARCH
 PEAK_F16_MFMA = 2516.6      # TFLOP/s, MI355X dense FP16 matrix peak (16x the f32 rate, same table)
 DTYPES = {"fp32": "fp32",
           "f16x3": "fp32 (layer GEMMs as 3x fp16-split MFMA, fp32 accumulate)",
-          "bf16": "bf16 layer GEMMs (fp32 accumulate; LN/attention/graph/DDIM fp32): tolerance study"}
+          "bf16": "bf16 MFMA operands for the layer GEMMs, attention's scores and P.V and the graph product "
+                  "(L_g as a bf16 hi+lo pair); fp32 accumulate; LayerNorm, softmax and DDIM fp32: tolerance study"}
 METRIC = "poses/sec (B=1024, 17j, K=50 DDIM) at 1/2/4/8 MI355X; MPJPE Δ vs ref"
 
 # BASELINE.json configs 2-5 (config 1 is the reference's own CPU case, timed as cpu_baseline).
@@ -281,8 +282,8 @@ def config3_parity(args, x_all, tgt_all, out_bf16, out_fp32):
     tg = tgt_all[:n]
     m_r = mpjpe_mm(ref, tg, 1)
     res = {"frames": n, "K": len(seq3), "T": CONFIGS[3]["T"], "mpjpe_ref_mm": round(m_r, 6), "oracle_s": round(cpu_s, 2),
-           "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs and of attention's score and "
-                   "P.V products; fp32 beside it on the same frames and schedule; the fp32 bar is 1e-4 mm"}
+           "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs, attention's score and "
+                   "P.V products and the graph product; fp32 beside it on the same frames and schedule; the fp32 bar is 1e-4 mm"}
     for name, o in (("bf16", out_bf16), ("fp32", out_fp32)):
         m_h = mpjpe_mm(o[:n], tg, 1)
         res[name] = {"mpjpe_hip_mm": round(m_h, 6), "mpjpe_delta_mm": float(f"{abs(m_h - m_r):.3e}"),
@@ -615,7 +616,7 @@ def rank_main(args):
                      "tolerance_mm": 1e-4, "pass": abs(m_h - m_r) <= 1e-4}
                 if gemm == "bf16":   # reduced precision: the delta IS the tolerance-study result
                     r.update({"tolerance_mm": None, "pass": None,
-                              "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs and of attention's score and P.V products; the fp32 bar is 1e-4 mm"})
+                              "note": "tolerance study (BASELINE config 3): bf16 operands of the layer GEMMs, attention's score and P.V products and the graph product; the fp32 bar is 1e-4 mm"})
                 return r
             result["parity"] = parity(out_main, args.gemm)
             for g, v in variants.items():

@@ -3,7 +3,7 @@
 #   gpurun --timeout 1200 -- 'bash tools/profile_r06.sh r06_vX'
 # GPU tests + smoke, bench lines (headline with the whole-batch CPU baseline, config 3, config 5 share,
 # f16x3), rocprofv3 kernel traces (headline, config 3, f16x3) and SQ passes of the low-precision launches,
-# phase traces.  Each GPU step has its own limit; the chain stops at the first failure.
+# FETCH_SIZE / WRITE_SIZE passes (headline and config 3, tools/traffic_from_pmc.py), phase traces.  Each GPU step has its own limit; the chain stops at the first failure.
 TAG=${1:-r06_vX}
 O=gpurun_out
 mkdir -p $O
@@ -38,6 +38,13 @@ step pmc_sq_f16x3
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/$O/${TAG}_f16x3_pmc_sq -o run -- python3 $R/bench.py --gemm f16x3 --steps 3 --warmup 1 --no-cpu --no-variants > /dev/null 2>&1 || exit 11
 step pmc_sq2_f16x3
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d $R/$O/${TAG}_f16x3_pmc_sq2 -o run -- python3 $R/bench.py --gemm f16x3 --steps 3 --warmup 1 --no-cpu --no-variants > /dev/null 2>&1 || exit 12
+for cfg in "fp32:" "c3:--config 3"; do
+  n=${cfg%%:*}; a=${cfg#*:}
+  for c in FETCH_SIZE WRITE_SIZE; do
+    step pmc_${c}_$n
+    timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $R/$O/${TAG}_${n}_pmc_$c -o run -- python3 $R/bench.py $a --steps 3 --warmup 1 --no-cpu --no-variants > /dev/null 2>&1 || exit 16
+  done
+done
 cd $R
 step phase_trace
 timeout -k 10 120 python3 tools/phase_trace.py --run > $O/${TAG}_phase_trace.txt 2>&1 || exit 13
