@@ -1,6 +1,7 @@
-"""Copy one tools/profile_r05.sh run from gpurun_out/ into profiles/ with the summaries the docs cite.
+"""Copy one tools/profile_r05.sh / profile_r06.sh run from gpurun_out/ into profiles/ with the summaries the docs cite.
 
-  python tools/collect_profile.py TAG        # e.g. r05_v31
+  python tools/collect_profile.py TAG        # e.g. r05_v31, r06_v7
+(profile_r06.sh's FETCH_SIZE / WRITE_SIZE passes are folded by tools/traffic_from_pmc.py.)
 
 Per kernel trace (headline fp32, config-3 bf16, f16x3): the sampler kernel's per-dispatch durations
 (rocprofv3 --kernel-trace), their mean over the timed dispatches (the last `steps` of them), the bench line
